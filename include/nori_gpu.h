@@ -1,0 +1,223 @@
+/*
+ * nori_gpu.h -- C ABI of the MI355X wavefront path tracer (libnori_gpu.so).
+ *
+ * This is the drop-in boundary for Nori's render path.  The reference binds
+ * the path through C++ virtuals, not an FFI; each entry point below names the
+ * reference interface it replaces (paths relative to the reference checkout):
+ *
+ *   nori_scene_load_xml   <- loadFromXML()                src/parser.cpp:28-338
+ *                            + NoriObjectFactory::createInstance  include/nori/object.h:160-165
+ *                            + Scene::activate()          src/scene.cpp:43-61
+ *   nori_gpu_create       <- Scene::activate's BVH::build src/bvh.cpp:329-382 (flatten + upload)
+ *   nori_gpu_render       <- RenderThread::renderScene's pass loop
+ *                            src/render.cpp:173-250 (tbb::parallel_for over blocks,
+ *                            renderBlock render.cpp:80-133, Integrator::Li
+ *                            include/nori/integrator.h:55, ImageBlock::put
+ *                            src/block.cpp:93-133)
+ *   nori_gpu_trace        <- Scene::rayIntersect(ray, its) / rayIntersect(ray)
+ *                            include/nori/scene.h:93-115 -> BVH::rayIntersect src/bvh.cpp:404-462
+ *   nori_gpu_cancel       <- RenderThread::stopRendering  src/render.cpp:63-71
+ *   nori_gpu_progress     <- RenderThread::getProgress    src/render.cpp:73-78
+ *   nori_film_develop     <- ImageBlock::toBitmap         src/block.cpp:76-82
+ *   nori_write_exr        <- Bitmap::save                 src/bitmap.cpp:82-107
+ *
+ * Rules of the ABI: plain C types only, no exceptions cross it, every call
+ * returns an int status (NORI_OK = 0, negative = error) and the message of
+ * the last failure on the calling thread is nori_gpu_last_error().  All
+ * scene arrays are copied at nori_gpu_create(); the caller owns output
+ * buffers.  Arithmetic on the path is fp32 (Eigen float in the reference).
+ */
+#ifndef NORI_GPU_H
+#define NORI_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NORI_GPU_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define NORI_OK               0
+#define NORI_ERR_INVALID     -1   /* bad argument                        */
+#define NORI_ERR_IO          -2   /* file could not be read / written    */
+#define NORI_ERR_PARSE       -3   /* XML / OBJ syntax or property error  */
+#define NORI_ERR_UNSUPPORTED -4   /* plugin outside this path's scope    */
+#define NORI_ERR_HIP         -5   /* HIP runtime failure / no device     */
+#define NORI_ERR_CANCELLED   -6   /* nori_gpu_cancel() was honoured      */
+#define NORI_ERR_OOM         -7   /* device allocation failed            */
+
+/* ---- plugin kinds (XML `type` names in comments) ------------------------ */
+enum { NORI_SHAPE_MESH = 0 /* "obj" */, NORI_SHAPE_SPHERE = 1 /* "sphere" */ };
+enum {
+    NORI_BSDF_DIFFUSE = 0,    /* "diffuse"    src/diffuse.cpp    */
+    NORI_BSDF_MIRROR = 1,     /* "mirror"     src/mirror.cpp     */
+    NORI_BSDF_DIELECTRIC = 2, /* "dielectric" src/dielectric.cpp */
+    NORI_BSDF_MICROFACET = 3, /* "microfacet" src/microfacet.cpp */
+    NORI_BSDF_DISNEY = 4      /* "disney"     src/disney.cpp     */
+};
+enum { NORI_EMITTER_AREA = 0 /* "area" */, NORI_EMITTER_ENVMAP = 1 /* "envmap" */ };
+enum {
+    NORI_INTEGRATOR_PATH_MATS = 0,  /* "path_mats"  src/path_mats.cpp  */
+    NORI_INTEGRATOR_PATH_MIS = 1,   /* "path_mis"   src/path_mis.cpp   */
+    NORI_INTEGRATOR_VOLUMETRIC = 2  /* "volumetric" src/volumetric.cpp */
+};
+enum {
+    NORI_FILTER_GAUSSIAN = 0, NORI_FILTER_MITCHELL = 1, NORI_FILTER_TENT = 2,
+    NORI_FILTER_BOX = 3, NORI_FILTER_WINDOWED = 4     /* src/rfilter.cpp */
+};
+/* Random-number stream layout.
+ *  WAVE : one pcg32 stream per (pass k, pixel) sample -- counter based, the
+ *         layout the GPU uses; identical in the CPU oracle.
+ *  BLOCK: the reference's layout: one stream per 32x32 block seeded with
+ *         seed(offset.x, offset.y) and consumed serially over pixels and
+ *         passes (src/independent.cpp:48-67, src/render.cpp:212-216).  CPU
+ *         oracle only. */
+enum { NORI_RNG_WAVE = 0, NORI_RNG_BLOCK = 1 };
+
+#define NORI_BLOCK_SIZE 32           /* include/nori/block.h:30   */
+#define NORI_FILTER_RESOLUTION 32    /* include/nori/rfilter.h:25 */
+#define NORI_EPSILON 1e-4f           /* include/nori/common.h:52  */
+
+/* ---- flattened scene (POD) ---------------------------------------------- */
+typedef struct nori_shape_desc {
+    int32_t type;                 /* NORI_SHAPE_*                              */
+    uint32_t tri_offset;          /* mesh: first triangle in indices[]         */
+    uint32_t tri_count;           /* mesh: triangle count (sphere: 1 primitive) */
+    uint32_t vtx_offset;          /* mesh: first vertex in positions[]         */
+    uint32_t vtx_count;
+    int32_t has_normals;          /* mesh: per-vertex normals present          */
+    int32_t has_uvs;              /* mesh: per-vertex uvs present              */
+    float center[3];              /* sphere                                    */
+    float radius;                 /* sphere                                    */
+    int32_t bsdf;                 /* index into bsdfs[]                         */
+    int32_t emitter;              /* index into emitters[] or -1               */
+} nori_shape_desc;
+
+typedef struct nori_bsdf_desc {
+    int32_t type;                 /* NORI_BSDF_*                               */
+    float albedo[3];              /* diffuse: constant_color albedo (def 0.5)  */
+    float int_ior, ext_ior;       /* dielectric / microfacet                   */
+    float alpha;                  /* microfacet                                */
+    float kd[3];                  /* microfacet                                */
+    float base_color[3];          /* disney                                    */
+    float metallic, specular, roughness, sheen, sheen_tint, specular_tint;
+} nori_bsdf_desc;
+
+typedef struct nori_emitter_desc {
+    int32_t type;                 /* NORI_EMITTER_*                            */
+    int32_t shape;                /* attached shape index (area, envmap)       */
+    float radiance[3];            /* area                                      */
+    float weight;                 /* envmap                                    */
+    float lum_scale[3];           /* envmap luminanceScale                     */
+    int32_t env_rows, env_cols;   /* envmap: Bitmap rows x cols                */
+    const float *env_rgb;         /* envmap: rows*cols*3 floats (row-major)    */
+} nori_emitter_desc;
+
+typedef struct nori_camera_desc {
+    int32_t width, height;
+    float fov, near_clip, far_clip;
+    float camera_to_world[16];    /* row-major 4x4                             */
+    float sample_to_camera[16];   /* row-major 4x4 (perspective.cpp:53-82)     */
+    int32_t filter_type;          /* NORI_FILTER_*                             */
+    float filter_radius;
+    float filter_p0, filter_p1;   /* gaussian: stddev | mitchell: B, C | windowed: tau */
+} nori_camera_desc;
+
+typedef struct nori_medium_desc {
+    int32_t present;
+    float sigma_a[3], sigma_s[3];
+    float box_min[3], box_max[3]; /* origin -/+ |box_size| (medium.cpp:16-18)  */
+} nori_medium_desc;
+
+typedef struct nori_scene_desc {
+    uint32_t abi_version;
+    uint32_t num_vertices;
+    const float *positions;       /* 3*num_vertices                            */
+    const float *normals;         /* 3*num_vertices (zeros where absent)       */
+    const float *uvs;             /* 2*num_vertices (zeros where absent)       */
+    uint32_t num_triangles;
+    const uint32_t *indices;      /* 3*num_triangles, global vertex ids        */
+    uint32_t num_shapes;
+    const nori_shape_desc *shapes;      /* BVH primitive order = shape order  */
+    uint32_t num_bsdfs;
+    const nori_bsdf_desc *bsdfs;
+    uint32_t num_emitters;
+    const nori_emitter_desc *emitters;  /* Scene::addChild order (scene.cpp:63-104) */
+    nori_camera_desc camera;
+    nori_medium_desc medium;
+    int32_t integrator;           /* NORI_INTEGRATOR_*                          */
+    uint32_t sample_count;        /* independent sampler sampleCount = spp      */
+} nori_scene_desc;
+
+/* ---- host-side scene loading (the plugin boundary) ----------------------- */
+typedef struct nori_scene nori_scene;
+
+/* Parse a Nori XML scene (same tags, `type` names, property names and
+ * defaults as the reference).  width/height/spp > 0 override the XML. */
+int nori_scene_load_xml(const char *path, int width, int height, int spp, nori_scene **out);
+const nori_scene_desc *nori_scene_get_desc(const nori_scene *scene);
+void nori_scene_free(nori_scene *scene);
+
+/* Film border (ceil(radius - 0.5), block.cpp:57) and the 33-entry filter
+ * table (block.cpp:59-64) for the scene's reconstruction filter. */
+int nori_film_border(const nori_scene_desc *scene);
+int nori_filter_table(const nori_scene_desc *scene, float table[NORI_FILTER_RESOLUTION + 1]);
+/* RGBW film (H+2b)x(W+2b)x4 -> RGB bitmap HxWx3 divided by the filter weight
+ * (ImageBlock::toBitmap, Color4f::divideByFilterWeight color.h:113-118). */
+int nori_film_develop(const nori_scene_desc *scene, const float *rgbw, float *rgb);
+/* Write an RGB float image as an uncompressed scanline OpenEXR file. */
+int nori_write_exr(const char *path, const float *rgb, int width, int height);
+
+/* ---- GPU context ----------------------------------------------------------- */
+typedef struct nori_gpu_ctx nori_gpu_ctx;
+
+typedef struct nori_gpu_render_desc {
+    uint32_t pass_begin;          /* first sample pass k                        */
+    uint32_t pass_count;          /* passes to render (0 = scene spp)           */
+    uint32_t num_blocks;          /* 0 = every 32x32 block of the frame         */
+    const uint32_t *block_ids;    /* host array, id = by*nbx + bx (block.cpp:168) */
+    uint64_t seed;                /* stream seed mixed into every sample id     */
+    int32_t output_on_device;     /* rgbw_out is a device pointer on ctx device */
+    uint32_t path_pool;           /* paths in flight (0 = default)              */
+} nori_gpu_render_desc;
+
+typedef struct nori_gpu_stats {
+    uint64_t samples;             /* camera samples completed                   */
+    uint64_t invalid_samples;     /* NaN/Inf/negative radiance, dropped (block.cpp:94-98) */
+    uint64_t rays_closest;        /* extension rays traced                      */
+    uint64_t rays_shadow;         /* shadow rays traced                         */
+    uint64_t iterations;          /* wavefront iterations                       */
+    double ms_total;              /* render wall time (host timer)              */
+    double ms_extend, ms_shadow, ms_shade, ms_splat;  /* HIP-event kernel time  */
+} nori_gpu_stats;
+
+typedef struct nori_gpu_hit {
+    float t;                      /* +inf on miss                               */
+    int32_t prim;                 /* global primitive id (shape order), -1 miss */
+    float u, v;                   /* barycentrics (mesh)                        */
+} nori_gpu_hit;
+
+const char *nori_gpu_last_error(void);
+int nori_gpu_abi_version(void);
+int nori_gpu_device_count(int *count);
+int nori_gpu_create(const nori_scene_desc *scene, int device, nori_gpu_ctx **out);
+/* Render passes [pass_begin, pass_begin+pass_count) of the given blocks and
+ * ADD the filtered samples into rgbw_out ((H+2b)x(W+2b)x4 floats, caller
+ * owned, host or device memory).  Blocking. */
+int nori_gpu_render(nori_gpu_ctx *ctx, const nori_gpu_render_desc *desc,
+                    float *rgbw_out, nori_gpu_stats *stats);
+/* Trace n rays (host arrays; ray = o.xyz, mint, d.xyz, maxt) with the
+ * reference's BVH semantics: closest hit, or any hit when any_hit != 0. */
+int nori_gpu_trace(nori_gpu_ctx *ctx, const float *rays, uint32_t n, int any_hit,
+                   nori_gpu_hit *hits);
+int nori_gpu_cancel(nori_gpu_ctx *ctx);
+float nori_gpu_progress(const nori_gpu_ctx *ctx);
+void nori_gpu_destroy(nori_gpu_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NORI_GPU_H */

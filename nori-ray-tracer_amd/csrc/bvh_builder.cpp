@@ -1,0 +1,342 @@
+// bvh_builder.cpp -- host BVH construction for the device traversal kernels.
+//
+// Split selection restates BVH::build / BVHBuildTask (bvh.cpp:100-382):
+// 16-bin SAH along the node's largest axis above 32 primitives, a full
+// three-axis sweep below, T = I = 1 costs.  It runs serially and is
+// deterministic (centroid ties broken by primitive id, order-preserving
+// partition) -- the reference's TBB partition order is scheduling dependent.
+// The finished tree is re-emitted in the device layout of host_scene.h:
+// child boxes stored in the parent so one 64-byte fetch tests both children,
+// leaves inlined into the child reference.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+
+#include "host_scene.h"
+
+namespace nori {
+namespace {
+
+struct Box {
+    float mn[3], mx[3];
+    Box() {
+        for (int i = 0; i < 3; ++i) mn[i] = __builtin_inff(), mx[i] = -__builtin_inff();
+    }
+    void expand(const Box &b) {
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = std::fmin(mn[i], b.mn[i]);
+            mx[i] = std::fmax(mx[i], b.mx[i]);
+        }
+    }
+    void expand(const float *p) {
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = std::fmin(mn[i], p[i]);
+            mx[i] = std::fmax(mx[i], p[i]);
+        }
+    }
+    float area() const {  // bbox.h:87-100
+        float d[3] = {mx[0] - mn[0], mx[1] - mn[1], mx[2] - mn[2]};
+        float r = 0.0f;
+        for (int i = 0; i < 3; ++i) {
+            float t = 1.0f;
+            for (int j = 0; j < 3; ++j)
+                if (i != j) t *= d[j];
+            r += t;
+        }
+        return 2.0f * r;
+    }
+    int largest_axis() const {  // bbox.h:308-317
+        float e[3] = {mx[0] - mn[0], mx[1] - mn[1], mx[2] - mn[2]};
+        if (e[0] >= e[1] && e[0] >= e[2]) return 0;
+        if (e[1] >= e[0] && e[1] >= e[2]) return 1;
+        return 2;
+    }
+};
+
+struct RefNode {  // bvh.h:127-164 semantics
+    bool leaf = false, used = false;
+    uint32_t a = 0;  // leaf: size | inner: axis
+    uint32_t b = 0;  // leaf: start | inner: right child
+    Box box;
+};
+
+struct Builder {
+    std::vector<RefNode> nodes;
+    std::vector<uint32_t> idx, temp;
+    std::vector<float> cent;  // 3 per prim
+    std::vector<Box> pbox;
+
+    void sort_axis(uint32_t *s, uint32_t n, int axis) {
+        std::sort(s, s + n, [&](uint32_t a, uint32_t b) {
+            float ca = cent[3 * a + axis], cb = cent[3 * b + axis];
+            if (ca < cb) return true;
+            if (cb < ca) return false;
+            return a < b;
+        });
+    }
+    void serial(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp) {  // bvh.cpp:236-305
+        RefNode &node = nodes[ni];
+        node.used = true;
+        uint32_t size = (uint32_t)(end - start);
+        float best_cost = (float)1 * size;
+        int64_t best_index = -1, best_axis = -1;
+        float *left_areas = reinterpret_cast<float *>(tmp);
+        for (int axis = 0; axis < 3; ++axis) {
+            sort_axis(start, size, axis);
+            Box bb;
+            for (uint32_t i = 0; i < size; ++i) {
+                bb.expand(pbox[start[i]]);
+                left_areas[i] = bb.area();
+            }
+            if (axis == 0) node.box = bb;
+            bb = Box();
+            float tri_factor = 1 / node.box.area();
+            for (uint32_t i = size - 1; i >= 1; --i) {
+                bb.expand(pbox[start[i]]);
+                float sah = 2.0f * 1 + tri_factor * ((float)i * left_areas[i - 1] + (float)(size - i) * bb.area());
+                if (sah < best_cost) {
+                    best_cost = sah;
+                    best_index = i;
+                    best_axis = axis;
+                }
+            }
+        }
+        if (best_index == -1) {
+            node.leaf = true;
+            node.a = size;
+            node.b = (uint32_t)(start - idx.data());
+            return;
+        }
+        sort_axis(start, size, (int)best_axis);
+        uint32_t lc = (uint32_t)best_index, l = ni + 1, r = ni + 2 * lc;
+        node.leaf = false;
+        node.a = (uint32_t)best_axis;
+        node.b = r;
+        serial(l, start, start + lc, tmp);
+        serial(r, start + lc, end, tmp + lc);
+    }
+    void task(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp) {  // bvh.cpp:100-233
+        for (;;) {
+            uint32_t size = (uint32_t)(end - start);
+            RefNode &node = nodes[ni];
+            node.used = true;
+            if (size < 32) {
+                serial(ni, start, end, tmp);
+                return;
+            }
+            int axis = node.box.largest_axis();
+            float mn = node.box.mn[axis], mx = node.box.mx[axis], inv_bin = 16 / (mx - mn);
+            uint32_t counts[16] = {0};
+            Box bins[16];
+            for (uint32_t i = 0; i < size; ++i) {
+                uint32_t f = start[i];
+                int index = (int)((cent[3 * f + axis] - mn) * inv_bin);
+                index = std::min(std::max(index, 0), 15);
+                counts[index]++;
+                bins[index].expand(pbox[f]);
+            }
+            Box left[16];
+            left[0] = bins[0];
+            for (int i = 1; i < 16; ++i) {
+                counts[i] += counts[i - 1];
+                left[i] = left[i - 1];
+                left[i].expand(bins[i]);
+            }
+            Box right = bins[15], best_right;
+            int64_t best_index = -1;
+            float best_cost = (float)1 * size, tri_factor = (float)1 / node.box.area();
+            for (int i = 14; i >= 0; --i) {
+                uint32_t pl = counts[i], pr = size - counts[i];
+                float sah = 2.0f * 1 + tri_factor * ((float)pl * left[i].area() + (float)pr * right.area());
+                if (sah < best_cost) {
+                    best_cost = sah;
+                    best_index = i;
+                    best_right = right;
+                }
+                right.expand(bins[i]);
+            }
+            if (best_index == -1) {
+                serial(ni, start, end, tmp);
+                return;
+            }
+            uint32_t lc = counts[best_index], l = ni + 1, r = ni + 2 * lc;
+            nodes[l].box = left[best_index];
+            nodes[r].box = best_right;
+            node.leaf = false;
+            node.a = (uint32_t)axis;
+            node.b = r;
+            uint32_t il = 0, ir = lc;
+            for (uint32_t i = 0; i < size; ++i) {
+                uint32_t f = start[i];
+                int index = (int)((cent[3 * f + axis] - mn) * inv_bin);
+                if (index <= best_index) tmp[il++] = f;
+                else tmp[ir++] = f;
+            }
+            std::memcpy(start, tmp, size * sizeof(uint32_t));
+            task(r, start + lc, end, tmp + lc);
+            ni = l;
+            end = start + lc;
+        }
+    }
+    float statistics(uint32_t ni, uint32_t &count) const {  // bvh.cpp:384-402
+        const RefNode &n = nodes[ni];
+        if (n.leaf) {
+            count = 1;
+            return (float)n.a;
+        }
+        uint32_t cl, cr;
+        float sl = statistics(ni + 1, cl), sr = statistics(n.b, cr);
+        count = cl + cr + 1;
+        return 2 + (nodes[ni + 1].box.area() * sl + nodes[n.b].box.area() * sr) / n.box.area();
+    }
+};
+
+}  // namespace
+
+void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const float root_max[3], DeviceBvh &out) {
+    // primitive table in shape order (BVH::addShape, bvh.cpp:307-311)
+    std::vector<uint32_t> prim_shape;
+    std::vector<uint32_t> prim_local;
+    for (uint32_t s = 0; s < d.num_shapes; ++s) {
+        uint32_t n = d.shapes[s].type == NORI_SHAPE_SPHERE ? 1 : d.shapes[s].tri_count;
+        for (uint32_t i = 0; i < n; ++i) {
+            prim_shape.push_back(s);
+            prim_local.push_back(i);
+        }
+    }
+    uint32_t n = (uint32_t)prim_shape.size();
+    out = DeviceBvh();
+    if (n == 0) throw NoriException(NORI_ERR_INVALID, "scene has no primitives");
+    if (n >= (1u << 25)) throw NoriException(NORI_ERR_UNSUPPORTED, "more than 2^25 primitives");
+    Builder b;
+    b.cent.resize(3 * (size_t)n);
+    b.pbox.resize(n);
+    auto vtx = [&](uint32_t i) { return d.positions + 3 * (size_t)i; };
+    for (uint32_t p = 0; p < n; ++p) {
+        const nori_shape_desc &sh = d.shapes[prim_shape[p]];
+        if (sh.type == NORI_SHAPE_SPHERE) {  // sphere.cpp:32-41
+            float lo[3], hi[3];
+            for (int k = 0; k < 3; ++k) lo[k] = sh.center[k] - sh.radius, hi[k] = sh.center[k] + sh.radius;
+            b.pbox[p].expand(lo);
+            b.pbox[p].expand(hi);
+            for (int k = 0; k < 3; ++k) b.cent[3 * p + k] = sh.center[k];
+        } else {  // mesh.cpp:172-184
+            const uint32_t *f = d.indices + 3 * (size_t)(sh.tri_offset + prim_local[p]);
+            const float *p0 = vtx(f[0]), *p1 = vtx(f[1]), *p2 = vtx(f[2]);
+            b.pbox[p].expand(p0);
+            b.pbox[p].expand(p1);
+            b.pbox[p].expand(p2);
+            for (int k = 0; k < 3; ++k) b.cent[3 * p + k] = (1.0f / 3.0f) * ((p0[k] + p1[k]) + p2[k]);
+        }
+    }
+    b.nodes.assign(2 * (size_t)n, RefNode());
+    b.idx.resize(n);
+    b.temp.resize(n);
+    for (uint32_t i = 0; i < n; ++i) b.idx[i] = i;
+    for (int k = 0; k < 3; ++k) b.nodes[0].box.mn[k] = root_min[k], b.nodes[0].box.mx[k] = root_max[k];
+    b.task(0, b.idx.data(), b.idx.data() + n, b.temp.data());
+    uint32_t cnt = 0;
+    out.sah_cost = b.statistics(0, cnt);
+    out.ref_nodes = cnt;
+
+    // ---- primitive records in leaf order
+    out.prims.assign(12 * (size_t)n, 0.0f);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t p = b.idx[i];
+        float *r = &out.prims[12 * (size_t)i];
+        const nori_shape_desc &sh = d.shapes[prim_shape[p]];
+        uint32_t pid = p;
+        if (sh.type == NORI_SHAPE_SPHERE) {
+            r[0] = sh.center[0]; r[1] = sh.center[1]; r[2] = sh.center[2];
+            r[4] = sh.radius;
+            uint32_t one = 1;
+            std::memcpy(&r[7], &one, 4);
+        } else {
+            const uint32_t *f = d.indices + 3 * (size_t)(sh.tri_offset + prim_local[p]);
+            const float *p0 = vtx(f[0]), *p1 = vtx(f[1]), *p2 = vtx(f[2]);
+            for (int k = 0; k < 3; ++k) {
+                r[k] = p0[k];
+                r[4 + k] = p1[k] - p0[k];  // edge1 (mesh.cpp:88)
+                r[8 + k] = p2[k] - p0[k];  // edge2
+            }
+        }
+        std::memcpy(&r[3], &pid, 4);
+    }
+
+    // ---- device nodes: DFS over the reference tree
+    struct Child {
+        uint32_t ref;
+        Box box;
+    };
+    std::vector<float> &nodes = out.nodes;
+    uint32_t max_depth = 0;
+    // returns the child ref for reference node `ri`; leaves larger than
+    // kLeafMaxPrims are split into a chain of inner nodes (same primitive set).
+    std::function<Child(uint32_t, uint32_t, uint32_t, uint32_t)> leaf_ref = [&](uint32_t start, uint32_t count,
+                                                                              uint32_t depth, uint32_t) -> Child {
+        Child c;
+        for (uint32_t i = start; i < start + count; ++i) c.box.expand(b.pbox[b.idx[i]]);
+        if (count <= kLeafMaxPrims) {
+            c.ref = kLeafBit | ((count - 1) << 25) | start;
+            return c;
+        }
+        uint32_t me = (uint32_t)(nodes.size() / 16);
+        nodes.resize(nodes.size() + 16, 0.0f);
+        max_depth = std::max(max_depth, depth + 1);
+        uint32_t half = count / 2;
+        Child l = leaf_ref(start, half, depth + 1, 0), r = leaf_ref(start + half, count - half, depth + 1, 0);
+        float *nd = &nodes[16 * (size_t)me];
+        for (int k = 0; k < 3; ++k) {
+            nd[k] = l.box.mn[k]; nd[4 + k] = l.box.mx[k];
+            nd[8 + k] = r.box.mn[k]; nd[12 + k] = r.box.mx[k];
+        }
+        std::memcpy(&nd[3], &l.ref, 4);
+        std::memcpy(&nd[7], &r.ref, 4);
+        c.ref = me;
+        return c;
+    };
+    std::function<Child(uint32_t, uint32_t)> emit = [&](uint32_t ri, uint32_t depth) -> Child {
+        const RefNode &rn = b.nodes[ri];
+        if (rn.leaf) {
+            Child c = leaf_ref(rn.b, rn.a, depth, 0);
+            c.box = rn.box;
+            return c;
+        }
+        uint32_t me = (uint32_t)(nodes.size() / 16);
+        nodes.resize(nodes.size() + 16, 0.0f);
+        max_depth = std::max(max_depth, depth + 1);
+        Child l = emit(ri + 1, depth + 1), r = emit(rn.b, depth + 1);
+        float *nd = &nodes[16 * (size_t)me];
+        for (int k = 0; k < 3; ++k) {
+            nd[k] = b.nodes[ri + 1].box.mn[k]; nd[4 + k] = b.nodes[ri + 1].box.mx[k];
+            nd[8 + k] = b.nodes[rn.b].box.mn[k]; nd[12 + k] = b.nodes[rn.b].box.mx[k];
+        }
+        std::memcpy(&nd[3], &l.ref, 4);
+        std::memcpy(&nd[7], &r.ref, 4);
+        Child c;
+        c.ref = me;
+        c.box = rn.box;
+        return c;
+    };
+    if (b.nodes[0].leaf) {
+        // root leaf: one inner node whose right child box is empty
+        nodes.resize(16, 0.0f);
+        Child l = leaf_ref(b.nodes[0].b, b.nodes[0].a, 1, 0);
+        float *nd = &nodes[0];
+        for (int k = 0; k < 3; ++k) {
+            nd[k] = b.nodes[0].box.mn[k]; nd[4 + k] = b.nodes[0].box.mx[k];
+            nd[8 + k] = __builtin_inff(); nd[12 + k] = -__builtin_inff();
+        }
+        std::memcpy(&nd[3], &l.ref, 4);
+        uint32_t empty = kLeafBit;  // never visited: its box is empty
+        std::memcpy(&nd[7], &empty, 4);
+        max_depth = std::max<uint32_t>(max_depth, 1);
+    } else {
+        emit(0, 0);
+    }
+    out.num_nodes = (uint32_t)(nodes.size() / 16);
+    out.depth = max_depth;
+}
+
+}  // namespace nori

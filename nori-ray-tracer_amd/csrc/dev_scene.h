@@ -1,0 +1,100 @@
+// dev_scene.h -- device-resident scene and wavefront queue layouts.
+//
+// HBM layout (all arrays 16-byte aligned, structure-of-arrays so a wave's
+// 64 lanes read/write 64 consecutive 16-byte records = 1 KiB per access):
+//   nodes      float4[4*N]   BVH, 64 B per inner node (host_scene.h)
+//   prims      float4[3*P]   48 B per primitive in leaf order
+//   tri_vidx   uint32[3*P]   vertex ids per global primitive (shading)
+//   pos, nrm   float4[V]     vertex position / normal (w unused)
+//   prim_shape uint32[P]     global primitive -> shape
+//   cdf        float[]       per-mesh area CDFs (DiscretePDF, dpdf.h)
+// Path queues (two, ping-ponged) hold one path per entry:
+//   ray_o float4 (o.xyz, mint)   ray_d float4 (d.xyz, maxt)
+//   hit   float4 (t, prim, u, v) thr   float4 (beta.rgb, previous bsdf pdf | -1)
+//   rng   uint4 (pcg32 state, inc) work  uint32 (sample record index)
+// Shadow queue: ray_o, ray_d, payload float4 (contribution.rgb, work).
+// Sample records: float4 per camera sample (L.rgb, 0).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_math.h"
+
+namespace nori {
+
+struct DevShape {
+    int32_t type, bsdf, emitter, has_normals;
+    uint32_t prim_offset, prim_count, cdf_offset, pad;
+    float center[3], radius;
+    float area_norm;     // DiscretePDF::getNormalization (mesh) or sphere pdf
+    float pad2[3];
+};
+
+struct DevEmitter {
+    int32_t type, shape;
+    float radiance[3];
+    float pad[3];
+};
+
+struct DevScene {
+    const float4 *nodes;
+    const float4 *prims;
+    const uint32_t *tri_vidx;
+    const float4 *pos;
+    const float4 *nrm;
+    const uint32_t *prim_shape;
+    const DevShape *shapes;
+    const DevBsdf *bsdfs;
+    const DevEmitter *emitters;
+    const float *cdf;
+    uint32_t num_emitters;
+    uint32_t num_nodes;
+    int32_t W, H;
+    float invW, invH;
+    float s2c[16];
+    float c2w[16];
+    float near_clip, far_clip;
+    float filter[NORI_FILTER_RESOLUTION + 1];
+    float filter_radius, lookup;
+    int32_t border;
+    int32_t integrator;
+    // homogeneous medium (medium.cpp)
+    int32_t has_medium;
+    float mbox_min[3], mbox_max[3];
+    float sigma_t[3], albedo[3];
+};
+
+struct PathQueue {
+    float4 *ray_o;
+    float4 *ray_d;
+    float4 *hit;
+    float4 *thr;
+    uint4 *rng;     // pcg32 state (x,y) and increment (z,w)
+    uint32_t *work;
+};
+
+struct ShadowQueue {
+    float4 *ray_o;
+    float4 *ray_d;
+    float4 *payload;
+};
+
+// Work decomposition: work id w in [0, total) -> pass w / M, list entry w % M.
+struct WorkDesc {
+    uint64_t total;
+    uint32_t M;              // pixels in the selected blocks
+    uint32_t pass_begin;     // absolute pass of work id 0
+    const uint32_t *pixels;  // M entries, y*W + x, block-major
+    uint64_t seed;
+};
+
+// Device counters (one 256-byte line, zeroed per render).
+struct Counters {
+    uint32_t qcount[2];           // path queue sizes (ping-pong)
+    uint32_t shadow_count[2];     // shadow queue size (ping-pong by iteration parity)
+    unsigned long long next_work; // work ids handed out
+    unsigned long long rays_closest, rays_shadow, invalid;
+    unsigned long long pad[25];
+};
+
+}  // namespace nori

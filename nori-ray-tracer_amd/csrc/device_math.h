@@ -1,0 +1,354 @@
+// device_math.h -- fp32 vector math, pcg32, warps, frames, BSDFs and the area
+// emitter for the gfx950 kernels.  Each routine restates the reference function
+// cited beside it (paths relative to the reference checkout).  The file is
+// compiled with -ffp-contract=off so +,-,*,/ and sqrt round exactly as in the
+// reference's x86-64 build; transcendentals come from the ROCm device library
+// and may differ from glibc by a few ulp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nori_gpu.h"
+
+#define ND __device__ __forceinline__
+#define NHD __host__ __device__ __forceinline__
+
+namespace nori {
+
+constexpr float kPi = 3.14159265358979323846f;      // common.h:56 (float literal)
+constexpr float kInvPi = 0.31830988618379067154f;   // common.h:57
+constexpr float kInvFourPi = 0.07957747154594766788f;
+constexpr float kEps = NORI_EPSILON;                // common.h:52
+
+struct V3 {
+    float x, y, z;
+};
+NHD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+NHD V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+NHD V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+NHD V3 operator-(V3 a) { return V3{-a.x, -a.y, -a.z}; }
+NHD V3 operator*(V3 a, float s) { return V3{a.x * s, a.y * s, a.z * s}; }
+NHD V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+NHD V3 operator/(V3 a, float s) { return V3{a.x / s, a.y / s, a.z / s}; }
+// Eigen's redux order for 3-vectors: (a0 + a1) + a2
+NHD float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+NHD V3 cross(V3 a, V3 b) {
+    return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+NHD float norm(V3 a) { return sqrtf(dot(a, a)); }
+NHD V3 normalize(V3 a) { return a / norm(a); }  // MatrixBase::normalized()
+NHD float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
+NHD float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
+NHD float maxc(V3 a) { return smax(smax(a.x, a.y), a.z); }
+NHD bool is_zero(V3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+NHD float luminance(V3 c) {  // common.cpp:233-235
+    return c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f;
+}
+NHD float clampf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+ND V3 ld3(const float4 &f) { return V3{f.x, f.y, f.z}; }
+
+// ---------------------------------------------------------------- pcg32
+// ext/pcg32/pcg32.h:51-110.  The increment of a WAVE stream is derived from
+// its sample id, so a path only carries the 64-bit state.
+constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
+struct Pcg {
+    uint64_t state, inc;
+};
+NHD uint32_t pcg_next(Pcg &r) {
+    uint64_t old = r.state;
+    r.state = old * kPcgMult + r.inc;
+    uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((-rot) & 31));
+}
+NHD void pcg_seed(Pcg &r, uint64_t initstate, uint64_t initseq) {
+    r.state = 0u;
+    r.inc = (initseq << 1u) | 1u;
+    pcg_next(r);
+    r.state += initstate;
+    pcg_next(r);
+}
+NHD float pcg_float(Pcg &r) {
+    uint32_t u = (pcg_next(r) >> 9) | 0x3f800000u;
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f - 1.0f;
+}
+NHD uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+// WAVE stream of camera sample `sample_id` (same definition as the oracle).
+NHD void wave_seed(Pcg &r, uint64_t seed, uint64_t sample_id) {
+    pcg_seed(r, splitmix64(sample_id ^ seed), sample_id);
+}
+struct V2 {
+    float x, y;
+};
+// Sampler::next1D / next2D (independent.cpp:58-67): x drawn first.
+NHD float next1D(Pcg &r) { return pcg_float(r); }
+NHD V2 next2D(Pcg &r) {
+    V2 s;
+    s.x = pcg_float(r);
+    s.y = pcg_float(r);
+    return s;
+}
+
+// ---------------------------------------------------------------- frames
+struct Frame {
+    V3 s, t, n;
+};
+NHD Frame frame_from(V3 a) {  // frame.h:49-51 + coordinateSystem common.cpp:274-283
+    Frame f;
+    f.n = a;
+    if (fabsf(a.x) > fabsf(a.y)) {
+        float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
+        f.t = V3{a.z * invLen, 0.0f, -a.x * invLen};
+    } else {
+        float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
+        f.t = V3{0.0f, a.z * invLen, -a.y * invLen};
+    }
+    f.s = cross(f.t, a);
+    return f;
+}
+NHD V3 to_local(const Frame &f, V3 v) { return V3{dot(v, f.s), dot(v, f.t), dot(v, f.n)}; }
+NHD V3 to_world(const Frame &f, V3 v) { return (f.s * v.x + f.t * v.y) + f.n * v.z; }
+NHD float tan_theta(V3 v) {  // frame.h:77-82
+    float temp = 1 - v.z * v.z;
+    if (temp <= 0.0f) return 0.0f;
+    return sqrtf(temp) / v.z;
+}
+
+NHD float fresnel(float cosThetaI, float extIOR, float intIOR) {  // common.cpp:285-314
+    float etaI = extIOR, etaT = intIOR;
+    if (extIOR == intIOR) return 0.0f;
+    if (cosThetaI < 0.0f) {
+        float t = etaI;
+        etaI = etaT;
+        etaT = t;
+        cosThetaI = -cosThetaI;
+    }
+    float eta = etaI / etaT, sinThetaTSqr = eta * eta * (1 - cosThetaI * cosThetaI);
+    if (sinThetaTSqr > 1.0f) return 1.0f;
+    float cosThetaT = sqrtf(1.0f - sinThetaTSqr);
+    float Rs = (etaI * cosThetaI - etaT * cosThetaT) / (etaI * cosThetaI + etaT * cosThetaT);
+    float Rp = (etaT * cosThetaI - etaI * cosThetaT) / (etaT * cosThetaI + etaI * cosThetaT);
+    return (Rs * Rs + Rp * Rp) / 2.0f;
+}
+
+// ---------------------------------------------------------------- warps
+NHD V3 sq_cosine_hemisphere(V2 s) {  // warp.cpp:110-115
+    float theta = acosf(sqrtf(1 - (1 - s.x)));
+    float phi = 2.f * kPi * s.y;
+    float st = sinf(theta);
+    return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
+}
+NHD V3 sq_uniform_sphere(V2 s) {  // warp.cpp:86-91
+    float theta = acosf(1 - 2 * (1 - s.x));
+    float phi = 2.f * kPi * s.y;
+    float st = sinf(theta);
+    return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
+}
+NHD float sq_uniform_sphere_pdf(V3 v) {  // warp.cpp:93-96
+    return fabsf(norm(v) - 1.0f) < kEps ? 0.25f * kInvPi : 0.0f;
+}
+NHD V3 sq_beckmann(V2 s, float alpha) {  // warp.cpp:122-127 (pow(alpha,2) is double)
+    double a2 = (double)alpha * (double)alpha;
+    float theta = (float)atan(sqrt(-a2 * (double)logf(1 - s.x)));
+    float phi = 2 * kPi * s.y;
+    float st = sinf(theta);
+    return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
+}
+NHD V3 sq_uniform_triangle(V2 s) {  // warp.cpp:135-140
+    float su1 = sqrtf(s.x);
+    float u = 1.f - su1, v = s.y * su1;
+    return V3{u, v, 1.f - u - v};
+}
+NHD V3 sq_gtr2(V2 s, float alpha) {  // warp.cpp:180-185
+    float a2 = alpha * alpha;  // (float)pow(alpha,2): exact product rounded once
+    float theta = acosf(sqrtf((1.0f - s.x) / (1.0f + (a2 - 1.0f) * s.x)));
+    float phi = 2 * kPi * s.y;
+    float st = sinf(theta);
+    return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
+}
+NHD float sq_gtr2_pdf(V3 m, float alpha) {  // warp.cpp:187-193
+    float a2 = alpha * alpha;
+    float cosTheta = m.z;
+    double base = 1.0 + (double)(a2 - 1.0f) * ((double)cosTheta * (double)cosTheta);
+    float pdf = (float)((double)(a2 * cosTheta * kInvPi) / (base * base));
+    return (cosTheta >= 0 && fabsf(dot(m, m) - 1.0f) < 1.0f) ? pdf : 0.0f;
+}
+
+// ---------------------------------------------------------------- BSDFs
+enum { kMeasureUnknown = 0, kMeasureSolidAngle = 1, kMeasureDiscrete = 2 };  // common.h:199-203
+
+// Device BSDF record: desc values plus derived constants.
+struct DevBsdf {
+    int32_t type;
+    float albedo[3];
+    float int_ior, ext_ior, alpha, ks;
+    float kd[3];
+    float base[3];
+    float metallic, specular, roughness, sheen, sheen_tint, spec_tint, d_alpha;
+};
+
+struct BRec {
+    V3 wi, wo;
+    int measure;
+};
+
+ND float beckmann_D(const DevBsdf &b, V3 m) {  // microfacet.cpp:47-53
+    float temp = tan_theta(m) / b.alpha, ct = m.z, ct2 = ct * ct;
+    return expf(-temp * temp) / (kPi * b.alpha * b.alpha * ct2 * ct2);
+}
+ND float smith_G1(const DevBsdf &b, V3 v, V3 m) {  // microfacet.cpp:56-76
+    float tanTheta = tan_theta(v);
+    if (tanTheta == 0.0f) return 1.0f;
+    if (dot(m, v) * v.z <= 0) return 0.0f;
+    float a = 1.0f / (b.alpha * tanTheta);
+    if (a >= 1.6f) return 1.0f;
+    float a2 = a * a;
+    return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
+}
+ND float schlick(float u) {  // disney.cpp:25-29: pow(m, 5) in double
+    double m = (double)clampf_(1 - u, 0.0f, 1.0f);
+    double m2 = m * m;
+    return (float)(m2 * m2 * m);
+}
+ND float ggx(float NdotV, float alphaG) {  // disney.cpp:31-36
+    float a = alphaG * alphaG, b = NdotV * NdotV;
+    return 1 / (NdotV + sqrtf(a + b - a * b));
+}
+ND V3 lerp3(float t, V3 a, V3 c) { return a * (1.0f - t) + c * t; }  // disney.cpp:40-42
+
+ND V3 bsdf_eval(const DevBsdf &b, const BRec &r) {
+    switch (b.type) {
+    case NORI_BSDF_DIFFUSE:  // diffuse.cpp:72-82
+        if (r.measure != kMeasureSolidAngle || r.wi.z <= 0 || r.wo.z <= 0) return V3{0, 0, 0};
+        return V3{b.albedo[0], b.albedo[1], b.albedo[2]} * kInvPi;
+    case NORI_BSDF_MICROFACET: {  // microfacet.cpp:79-90
+        V3 n = normalize(r.wi + r.wo);
+        float D = beckmann_D(b, n);
+        float F = fresnel(dot(n, r.wi), b.ext_ior, b.int_ior);
+        float G = smith_G1(b, r.wi, n) * smith_G1(b, r.wo, n);
+        float den = 4.0f * r.wi.z * r.wo.z;
+        float spec = b.ks * D * F * G / den;
+        V3 d = V3{b.kd[0], b.kd[1], b.kd[2]} * kInvPi;
+        return V3{d.x + spec, d.y + spec, d.z + spec};
+    }
+    case NORI_BSDF_DISNEY: {  // disney.cpp:63-114
+        float NdotV = r.wi.z, NdotL = r.wo.z;
+        if (NdotV < 0 || NdotL < 0) return V3{0, 0, 0};
+        V3 wh = normalize(r.wi + r.wo);
+        float LdotH = dot(r.wo, wh), VdotH = dot(r.wi, wh);
+        V3 base = V3{b.base[0], b.base[1], b.base[2]};
+        float l = luminance(base);
+        V3 white = V3{1, 1, 1};
+        V3 ctint = (l > 0.f) ? V3{base.x / l, base.y / l, base.z / l} : white;
+        float smix = (float)((double)b.specular * 0.08);
+        V3 cspec = lerp3(b.metallic, lerp3(b.spec_tint, white, ctint) * smix, base);
+        float fd90 = (float)(0.5 + (double)(2 * b.roughness) * ((double)VdotH * (double)VdotH));
+        float fl = schlick(NdotL), fv = schlick(NdotV);
+        V3 diffuse = ((base * kInvPi) * (1.f + (fd90 - 1.f) * fl)) * (1.f + (fd90 - 1.f) * fv);
+        float alpha = smax(0.001f, b.roughness * b.roughness);
+        float Ds = sq_gtr2_pdf(wh, alpha);
+        float FH = schlick(LdotH);
+        V3 Fs = lerp3(FH, cspec, white);
+        float Gs = ggx(NdotL, alpha) * ggx(NdotV, alpha);
+        V3 specular = (Fs * Gs) * Ds;
+        V3 fsheen = lerp3(b.sheen_tint, white, ctint) * (FH * b.sheen);
+        return (diffuse + fsheen) * (1 - b.metallic) + specular;
+    }
+    default:  // mirror / dielectric: discrete lobes evaluate to zero
+        return V3{0, 0, 0};
+    }
+}
+
+ND float bsdf_pdf(const DevBsdf &b, const BRec &r) {
+    switch (b.type) {
+    case NORI_BSDF_DIFFUSE:  // diffuse.cpp:85-98
+        if (r.measure != kMeasureSolidAngle || r.wi.z <= 0 || r.wo.z <= 0) return 0.0f;
+        return kInvPi * r.wo.z;
+    case NORI_BSDF_MICROFACET: {  // microfacet.cpp:93-106
+        float c = r.wo.z;
+        if (c <= 0.0f) return 0.0f;
+        V3 n = normalize(r.wi + r.wo);
+        float mt = beckmann_D(b, n) * n.z / (4.0f * fabsf(dot(n, r.wo)));
+        return b.ks * mt + (1 - b.ks) * (c * kInvPi);
+    }
+    case NORI_BSDF_DISNEY: {  // disney.cpp:117-129
+        float c = r.wo.z;
+        if (c <= 0.0f) return 0.0f;
+        V3 n = normalize(r.wi + r.wo);
+        float mt = sq_gtr2_pdf(n, b.d_alpha) * n.z / (4.0f * fabsf(dot(n, r.wo)));
+        return (1 - b.metallic) * (c * kInvPi) + b.metallic * mt;
+    }
+    default:
+        return 0.0f;
+    }
+}
+
+// Returns the sample weight; r.wo / r.measure are set as the reference sets them.
+ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
+    switch (b.type) {
+    case NORI_BSDF_DIFFUSE:  // diffuse.cpp:101-116
+        if (r.wi.z <= 0) return V3{0, 0, 0};
+        r.measure = kMeasureSolidAngle;
+        r.wo = sq_cosine_hemisphere(s);
+        return V3{b.albedo[0], b.albedo[1], b.albedo[2]};
+    case NORI_BSDF_MIRROR:  // mirror.cpp:39-55
+        if (r.wi.z <= 0) return V3{0, 0, 0};
+        r.wo = V3{-r.wi.x, -r.wi.y, r.wi.z};
+        r.measure = kMeasureDiscrete;
+        return V3{1, 1, 1};
+    case NORI_BSDF_DIELECTRIC: {  // dielectric.cpp:45-73
+        float theta = r.wi.z;
+        V3 nv = V3{0, 0, 1.0f};
+        if (fresnel(theta, b.ext_ior, b.int_ior) > s.x) {
+            r.wo = V3{-r.wi.x, -r.wi.y, r.wi.z};
+        } else {
+            float factor = b.ext_ior / b.int_ior;
+            if (theta < 0.0f) {
+                factor = 1 / factor;
+                nv.z *= -1;
+            }
+            V3 part1 = (r.wi - nv * dot(r.wi, nv)) * (-factor);
+            double wn = (double)dot(r.wi, nv);
+            double rad = 1.0 - (double)factor * (double)factor * (1.0 - wn * wn);
+            V3 part2 = (-nv) * (float)sqrt(rad);
+            r.wo = normalize(part1 + part2);
+        }
+        r.measure = kMeasureDiscrete;
+        return V3{1, 1, 1};
+    }
+    case NORI_BSDF_MICROFACET: {  // microfacet.cpp:109-131
+        if (r.wi.z <= 0.0f) return V3{0, 0, 0};
+        if (s.x < b.ks) {
+            V3 n = sq_beckmann(V2{s.x / b.ks, s.y}, b.alpha);
+            r.wo = normalize(n * (2.0f * dot(r.wi, n)) - r.wi);
+        } else {
+            r.wo = sq_cosine_hemisphere(V2{(s.x - b.ks) / (1.f - b.ks), s.y});
+        }
+        float c = r.wo.z;
+        if (c <= 0.f) return V3{0, 0, 0};
+        return (bsdf_eval(b, r) * c) / bsdf_pdf(b, r);
+    }
+    case NORI_BSDF_DISNEY: {  // disney.cpp:132-155
+        if (r.wi.z <= 0.0f) return V3{0, 0, 0};
+        if (s.x <= b.metallic) {
+            V3 n = sq_gtr2(V2{s.x / b.metallic, s.y}, b.d_alpha);
+            r.wo = normalize(n * (2.0f * dot(r.wi, n)) - r.wi);
+        } else {
+            r.wo = sq_cosine_hemisphere(V2{(s.x - b.metallic) / (1 - b.metallic), s.y});
+        }
+        float c = r.wo.z;
+        if (c <= 0.0f) return V3{0, 0, 0};
+        return (bsdf_eval(b, r) * c) / bsdf_pdf(b, r);
+    }
+    }
+    return V3{0, 0, 0};
+}
+
+}  // namespace nori

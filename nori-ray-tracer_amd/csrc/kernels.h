@@ -1,0 +1,35 @@
+// kernels.h -- launch wrappers for the gfx950 kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev_scene.h"
+
+namespace nori {
+
+constexpr int kShadeBlock = 256;   // shade / regen work-group size
+constexpr int kTraceBlock = 128;   // traversal work-group size (LDS stack columns)
+constexpr int kSplatBlock = 256;
+
+struct SplatDesc {
+    uint32_t M;               // pixels per pass in the work list
+    uint32_t passes;          // passes in this chunk
+    uint32_t pass_begin;      // absolute pass of chunk pass 0
+    uint32_t passes_per_wg;   // passes folded by one work-group
+    const int4 *blocks;       // (ox, oy, bw | bh << 16, first list entry)
+    uint64_t seed;
+};
+
+// stack = LDS stack depth (8, 16, 32 or 64) chosen from the BVH depth.
+hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int any_hit, float4 *hits, int stack,
+                        hipStream_t st);
+hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
+                        Counters *C, int in_sel, int sh_sel, const WorkDesc &wd, float4 *rec, uint32_t pool,
+                        hipStream_t st);
+hipError_t launch_extend(const DevScene &S, const PathQueue &q, Counters *C, int q_sel, int reset_q, int reset_sh,
+                         uint32_t pool, int stack, hipStream_t st);
+hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, Counters *C, int sh_sel, float4 *rec,
+                         uint32_t pool, int stack, hipStream_t st);
+hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
+                        Counters *C, hipStream_t st);
+
+}  // namespace nori

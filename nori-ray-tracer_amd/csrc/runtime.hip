@@ -1,0 +1,628 @@
+// runtime.hip -- libnori_gpu host runtime and C ABI (include/nori_gpu.h).
+//
+// nori_gpu_render replaces RenderThread::renderScene's pass loop
+// (render.cpp:173-250): instead of spp sequential passes of a
+// tbb::parallel_for over 32x32 blocks, every (pass, pixel) sample of the
+// requested blocks becomes a work id; a pool of paths stays resident in HBM
+// and the shade kernel refills finished slots from a device work counter, so
+// the GPU stays full until the last sample.  Radiance accumulates per sample
+// record; after the pool drains, k_splat applies ImageBlock::put.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host_scene.h"
+#include "kernels.h"
+
+namespace nori {
+
+static thread_local std::string g_last_error;
+
+#define HIP_TRY(x)                                                                                       \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) throw NoriException(NORI_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes && p) return;
+        release();
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw NoriException(NORI_ERR_OOM, std::string("hipMalloc(") + std::to_string(n) + "): " + hipGetErrorString(e));
+        }
+        bytes = n;
+    }
+    template <class T> void upload(const std::vector<T> &v) {
+        ensure(v.size() * sizeof(T));
+        if (!v.empty()) HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+// rfilter.cpp -> tabulated filter (block.cpp:54-66)
+static float filter_eval(const nori_camera_desc &c, float x) {
+    switch (c.filter_type) {
+    case NORI_FILTER_GAUSSIAN: {
+        float alpha = -1.0f / (2.0f * c.filter_p0 * c.filter_p0);
+        float v = std::exp(alpha * x * x) - std::exp(alpha * c.filter_radius * c.filter_radius);
+        return 0.0f < v ? v : 0.0f;
+    }
+    case NORI_FILTER_MITCHELL: {
+        float B = c.filter_p0, C = c.filter_p1;
+        x = std::fabs(2.0f * x / c.filter_radius);
+        float x2 = x * x, x3 = x2 * x;
+        if (x < 1) return 1.0f / 6.0f * ((12 - 9 * B - 6 * C) * x3 + (-18 + 12 * B + 6 * C) * x2 + (6 - 2 * B));
+        if (x < 2) return 1.0f / 6.0f * ((-B - 6 * C) * x3 + (6 * B + 30 * C) * x2 + (-12 * B - 48 * C) * x + (8 * B + 24 * C));
+        return 0.0f;
+    }
+    case NORI_FILTER_TENT: {
+        float v = 1.0f - std::fabs(x);
+        return 0.0f < v ? v : 0.0f;
+    }
+    case NORI_FILTER_BOX: return 1.0f;
+    case NORI_FILTER_WINDOWED: {
+        x = std::fabs(x);
+        const float pi = 3.14159265358979323846f;
+        auto sinc = [&](float y) { return y < 1e-5f ? 1.0f : std::sin(pi * y) / (pi * y); };
+        return sinc(x) * sinc(x / c.filter_p0);
+    }
+    }
+    return 0.0f;
+}
+static int film_border(const nori_camera_desc &c) { return (int)std::ceil(c.filter_radius - 0.5f); }
+static void filter_table(const nori_camera_desc &c, float *t) {
+    for (int i = 0; i < NORI_FILTER_RESOLUTION; ++i) t[i] = filter_eval(c, (c.filter_radius * i) / NORI_FILTER_RESOLUTION);
+    t[NORI_FILTER_RESOLUTION] = 0.0f;
+}
+
+// BlockGenerator spiral (block.cpp:140-188)
+static std::vector<uint32_t> spiral_blocks(int W, int H) {
+    int nx = (int)std::ceil(W / (float)NORI_BLOCK_SIZE), ny = (int)std::ceil(H / (float)NORI_BLOCK_SIZE);
+    std::vector<uint32_t> out;
+    int left = nx * ny, dir = 0, bx = nx / 2, by = ny / 2, steps = 1, numSteps = 1;
+    while (left > 0) {
+        out.push_back((uint32_t)(by * nx + bx));
+        if (--left == 0) break;
+        do {
+            switch (dir) {
+            case 0: ++bx; break;
+            case 1: ++by; break;
+            case 2: --bx; break;
+            default: --by; break;
+            }
+            if (--steps == 0) {
+                dir = (dir + 1) % 4;
+                if (dir == 2 || dir == 0) ++numSteps;
+                steps = numSteps;
+            }
+        } while (bx < 0 || by < 0 || bx >= nx || by >= ny);
+    }
+    return out;
+}
+
+}  // namespace nori
+
+using namespace nori;
+
+struct nori_scene {
+    std::unique_ptr<HostScene> hs;
+};
+
+struct nori_gpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevScene S{};
+    nori_camera_desc cam{};
+    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf;
+    int stack = 8;
+    uint32_t bvh_depth = 0, bvh_nodes = 0, num_prims = 0;
+    size_t scene_bytes = 0;
+    std::atomic<int> cancel{0};
+    std::atomic<float> progress{1.0f};
+    // render state
+    DevBuf q[2][6], sq[3], rec, counters, pixels, blocks, film;
+    uint32_t pool_cap = 0;
+    uint32_t *pinned = nullptr;  // readback ring
+    std::vector<hipEvent_t> ring;
+    ~nori_gpu_ctx() {
+        for (auto e : ring) (void)hipEventDestroy(e);
+        if (pinned) (void)hipHostFree(pinned);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+int fail(int code, const std::string &m) {
+    g_last_error = m;
+    return code;
+}
+
+template <class F> int guarded(F &&f) {
+    try {
+        g_last_error.clear();
+        return f();
+    } catch (const NoriException &e) {
+        return fail(e.code, e.what());
+    } catch (const std::bad_alloc &) {
+        return fail(NORI_ERR_OOM, "host allocation failed");
+    } catch (const std::exception &e) {
+        return fail(NORI_ERR_INVALID, e.what());
+    }
+}
+
+void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
+    float rmin[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float rmax[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    auto expand = [&](float x, float y, float z) {
+        float p[3] = {x, y, z};
+        for (int k = 0; k < 3; ++k) {
+            rmin[k] = std::fmin(rmin[k], p[k]);
+            rmax[k] = std::fmax(rmax[k], p[k]);
+        }
+    };
+    std::vector<DevShape> shapes(d.num_shapes);
+    std::vector<uint32_t> prim_shape, tri_vidx;
+    std::vector<float> cdf;
+    uint32_t off = 0;
+    for (uint32_t s = 0; s < d.num_shapes; ++s) {
+        const nori_shape_desc &sd = d.shapes[s];
+        DevShape &ds = shapes[s];
+        std::memset(&ds, 0, sizeof(ds));
+        ds.type = sd.type;
+        ds.bsdf = sd.bsdf;
+        ds.emitter = sd.emitter;
+        ds.has_normals = sd.has_normals;
+        ds.prim_offset = off;
+        for (int k = 0; k < 3; ++k) ds.center[k] = sd.center[k];
+        ds.radius = sd.radius;
+        if (sd.bsdf < 0 || (uint32_t)sd.bsdf >= d.num_bsdfs) throw NoriException(NORI_ERR_INVALID, "shape without a valid bsdf");
+        if (sd.type == NORI_SHAPE_SPHERE) {
+            ds.prim_count = 1;
+            float inv = 1.f / sd.radius;  // sphere.cpp:99-104: pow(1/r, 2) * 1/(4 pi)
+            ds.area_norm = (float)((double)inv * (double)inv * (double)(0.25f * 0.31830988618379067154f));
+            prim_shape.push_back(s);
+            tri_vidx.insert(tri_vidx.end(), {0u, 0u, 0u});
+            expand(sd.center[0] - sd.radius, sd.center[1] - sd.radius, sd.center[2] - sd.radius);
+            expand(sd.center[0] + sd.radius, sd.center[1] + sd.radius, sd.center[2] + sd.radius);
+        } else if (sd.type == NORI_SHAPE_MESH) {
+            if ((uint64_t)sd.tri_offset + sd.tri_count > d.num_triangles || (uint64_t)sd.vtx_offset + sd.vtx_count > d.num_vertices)
+                throw NoriException(NORI_ERR_INVALID, "mesh range outside the scene arrays");
+            ds.prim_count = sd.tri_count;
+            ds.cdf_offset = (uint32_t)cdf.size();
+            // Mesh::activate area DiscretePDF (mesh.cpp:30-38, dpdf.h:58-91)
+            std::vector<float> c(sd.tri_count + 1);
+            c[0] = 0.0f;
+            for (uint32_t t = 0; t < sd.tri_count; ++t) {
+                const uint32_t *f = d.indices + 3 * (size_t)(sd.tri_offset + t);
+                for (int k = 0; k < 3; ++k)
+                    if (f[k] >= d.num_vertices) throw NoriException(NORI_ERR_INVALID, "vertex index out of range");
+                const float *p0 = d.positions + 3 * (size_t)f[0], *p1 = d.positions + 3 * (size_t)f[1], *p2 = d.positions + 3 * (size_t)f[2];
+                float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]}, e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};
+                float cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
+                float area = 0.5f * std::sqrt((cx * cx + cy * cy) + cz * cz);
+                c[t + 1] = c[t] + area;
+                prim_shape.push_back(s);
+                tri_vidx.insert(tri_vidx.end(), {f[0], f[1], f[2]});
+            }
+            float sum = c[sd.tri_count];
+            if (sum > 0) {
+                float norm = 1.0f / sum;
+                for (uint32_t t = 1; t <= sd.tri_count; ++t) c[t] *= norm;
+                c[sd.tri_count] = 1.0f;
+                ds.area_norm = norm;
+            } else {
+                ds.area_norm = 0.0f;
+            }
+            cdf.insert(cdf.end(), c.begin(), c.end());
+            for (uint32_t v = 0; v < sd.vtx_count; ++v) {
+                const float *p = d.positions + 3 * (size_t)(sd.vtx_offset + v);
+                expand(p[0], p[1], p[2]);
+            }
+        } else {
+            throw NoriException(NORI_ERR_INVALID, "unknown shape type");
+        }
+        off += ds.prim_count;
+    }
+    c.num_prims = off;
+    std::vector<DevBsdf> bsdfs(d.num_bsdfs);
+    for (uint32_t i = 0; i < d.num_bsdfs; ++i) {
+        const nori_bsdf_desc &b = d.bsdfs[i];
+        DevBsdf &o = bsdfs[i];
+        std::memset(&o, 0, sizeof(o));
+        o.type = b.type;
+        for (int k = 0; k < 3; ++k) o.albedo[k] = b.albedo[k], o.kd[k] = b.kd[k], o.base[k] = b.base_color[k];
+        o.int_ior = b.int_ior;
+        o.ext_ior = b.ext_ior;
+        o.alpha = b.alpha;
+        float mk = b.kd[0] < b.kd[1] ? b.kd[1] : b.kd[0];
+        mk = mk < b.kd[2] ? b.kd[2] : mk;
+        o.ks = 1 - mk;  // microfacet.cpp:45
+        o.metallic = b.metallic;
+        o.specular = b.specular;
+        o.roughness = b.roughness;
+        o.sheen = b.sheen;
+        o.sheen_tint = b.sheen_tint;
+        o.spec_tint = b.specular_tint;
+        double r2 = (double)b.roughness * (double)b.roughness;  // disney.cpp:59
+        o.d_alpha = (float)(r2 > 1e-3 ? r2 : 1e-3);
+        if (b.type < NORI_BSDF_DIFFUSE || b.type > NORI_BSDF_DISNEY) throw NoriException(NORI_ERR_INVALID, "unknown bsdf type");
+    }
+    std::vector<DevEmitter> emitters(d.num_emitters);
+    for (uint32_t i = 0; i < d.num_emitters; ++i) {
+        const nori_emitter_desc &e = d.emitters[i];
+        if (e.type != NORI_EMITTER_AREA) throw NoriException(NORI_ERR_UNSUPPORTED, "only area emitters are on the GPU path this round");
+        if (e.shape < 0 || (uint32_t)e.shape >= d.num_shapes) throw NoriException(NORI_ERR_INVALID, "emitter without a shape");
+        std::memset(&emitters[i], 0, sizeof(DevEmitter));
+        emitters[i].type = e.type;
+        emitters[i].shape = e.shape;
+        for (int k = 0; k < 3; ++k) emitters[i].radiance[k] = e.radiance[k];
+    }
+    if (d.num_emitters == 0) throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
+    if (d.integrator != NORI_INTEGRATOR_PATH_MIS && d.integrator != NORI_INTEGRATOR_PATH_MATS)
+        throw NoriException(NORI_ERR_UNSUPPORTED, "integrator not yet on the GPU path");
+
+    DeviceBvh bvh;
+    build_device_bvh(d, rmin, rmax, bvh);
+    c.bvh_depth = bvh.depth;
+    c.bvh_nodes = bvh.num_nodes;
+    if (bvh.depth <= 8) c.stack = 8;
+    else if (bvh.depth <= 16) c.stack = 16;
+    else if (bvh.depth <= 32) c.stack = 32;
+    else if (bvh.depth <= 64) c.stack = 64;
+    else throw NoriException(NORI_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+
+    std::vector<float> pos(4 * (size_t)d.num_vertices), nrm(4 * (size_t)d.num_vertices);
+    for (uint32_t v = 0; v < d.num_vertices; ++v)
+        for (int k = 0; k < 3; ++k) {
+            pos[4 * (size_t)v + k] = d.positions[3 * (size_t)v + k];
+            nrm[4 * (size_t)v + k] = d.normals ? d.normals[3 * (size_t)v + k] : 0.0f;
+        }
+    if (pos.empty()) pos.assign(4, 0.0f), nrm.assign(4, 0.0f);
+    if (cdf.empty()) cdf.assign(1, 0.0f);
+    c.nodes.upload(bvh.nodes);
+    c.prims.upload(bvh.prims);
+    c.tri_vidx.upload(tri_vidx);
+    c.pos.upload(pos);
+    c.nrm.upload(nrm);
+    c.prim_shape.upload(prim_shape);
+    c.shapes.upload(shapes);
+    c.bsdfs.upload(bsdfs);
+    c.emitters.upload(emitters);
+    c.cdf.upload(cdf);
+    c.scene_bytes = c.nodes.bytes + c.prims.bytes;
+
+    DevScene &S = c.S;
+    S.nodes = c.nodes.as<float4>();
+    S.prims = c.prims.as<float4>();
+    S.tri_vidx = c.tri_vidx.as<uint32_t>();
+    S.pos = c.pos.as<float4>();
+    S.nrm = c.nrm.as<float4>();
+    S.prim_shape = c.prim_shape.as<uint32_t>();
+    S.shapes = c.shapes.as<DevShape>();
+    S.bsdfs = c.bsdfs.as<DevBsdf>();
+    S.emitters = c.emitters.as<DevEmitter>();
+    S.cdf = c.cdf.as<float>();
+    S.num_emitters = d.num_emitters;
+    S.num_nodes = bvh.num_nodes;
+    const nori_camera_desc &cam = d.camera;
+    c.cam = cam;
+    if (cam.width <= 0 || cam.height <= 0) throw NoriException(NORI_ERR_INVALID, "bad output size");
+    S.W = cam.width;
+    S.H = cam.height;
+    S.invW = 1.0f / (float)cam.width;
+    S.invH = 1.0f / (float)cam.height;
+    std::memcpy(S.s2c, cam.sample_to_camera, sizeof(S.s2c));
+    std::memcpy(S.c2w, cam.camera_to_world, sizeof(S.c2w));
+    S.near_clip = cam.near_clip;
+    S.far_clip = cam.far_clip;
+    filter_table(cam, S.filter);
+    S.filter_radius = cam.filter_radius;
+    S.lookup = NORI_FILTER_RESOLUTION / cam.filter_radius;
+    S.border = film_border(cam);
+    if (S.border > 8) throw NoriException(NORI_ERR_UNSUPPORTED, "filter radius above 8.5 pixels");
+    S.integrator = d.integrator;
+    S.has_medium = d.medium.present;
+}
+
+void ensure_pool(nori_gpu_ctx &c, uint32_t pool) {
+    if (pool <= c.pool_cap) return;
+    for (int b = 0; b < 2; ++b) {
+        c.q[b][0].ensure(16 * (size_t)pool);
+        c.q[b][1].ensure(16 * (size_t)pool);
+        c.q[b][2].ensure(16 * (size_t)pool);
+        c.q[b][3].ensure(16 * (size_t)pool);
+        c.q[b][4].ensure(16 * (size_t)pool);
+        c.q[b][5].ensure(4 * (size_t)pool);
+    }
+    for (int k = 0; k < 3; ++k) c.sq[k].ensure(16 * (size_t)pool);
+    c.pool_cap = pool;
+}
+
+PathQueue queue_of(nori_gpu_ctx &c, int b) {
+    PathQueue q;
+    q.ray_o = c.q[b][0].as<float4>();
+    q.ray_d = c.q[b][1].as<float4>();
+    q.hit = c.q[b][2].as<float4>();
+    q.thr = c.q[b][3].as<float4>();
+    q.rng = c.q[b][4].as<uint4>();
+    q.work = c.q[b][5].as<uint32_t>();
+    return q;
+}
+
+constexpr int kRing = 16;     // readback ring entries
+constexpr int kLookahead = 6; // iterations queued ahead of the termination check
+
+struct Timers {
+    std::vector<hipEvent_t> ev;
+    size_t used = 0;
+    hipEvent_t get() {
+        if (used == ev.size()) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            ev.push_back(e);
+        }
+        return ev[used++];
+    }
+    ~Timers() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nori_gpu_stats *stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(c.device));
+    const DevScene &S = c.S;
+    const int W = S.W, H = S.H, B = S.border;
+    const int nbx = (int)std::ceil(W / (float)NORI_BLOCK_SIZE), nby = (int)std::ceil(H / (float)NORI_BLOCK_SIZE);
+    std::vector<uint32_t> order = spiral_blocks(W, H);
+    if (rd.num_blocks) {
+        std::vector<char> want((size_t)nbx * nby, 0);
+        for (uint32_t i = 0; i < rd.num_blocks; ++i) {
+            if (rd.block_ids[i] >= (uint32_t)(nbx * nby)) throw NoriException(NORI_ERR_INVALID, "block id out of range");
+            want[rd.block_ids[i]] = 1;
+        }
+        std::vector<uint32_t> sel;
+        for (uint32_t b : order)
+            if (want[b]) sel.push_back(b);
+        order.swap(sel);
+    }
+    // block-major pixel list (camera samples of one block are adjacent work ids)
+    std::vector<uint32_t> pixels;
+    std::vector<int4> blocks;
+    for (uint32_t b : order) {
+        int bx = (int)(b % (uint32_t)nbx), by = (int)(b / (uint32_t)nbx);
+        int ox = bx * NORI_BLOCK_SIZE, oy = by * NORI_BLOCK_SIZE;
+        int bw = std::min(NORI_BLOCK_SIZE, W - ox), bh = std::min(NORI_BLOCK_SIZE, H - oy);
+        blocks.push_back(make_int4(ox, oy, bw | (bh << 16), (int)pixels.size()));
+        for (int y = 0; y < bh; ++y)
+            for (int x = 0; x < bw; ++x) pixels.push_back((uint32_t)((oy + y) * W + (ox + x)));
+    }
+    const uint32_t M = (uint32_t)pixels.size();
+    const uint32_t passes = rd.pass_count ? rd.pass_count : 0;
+    if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
+    uint32_t pool = rd.path_pool ? rd.path_pool : (1u << 21);
+    pool = (pool + 255) / 256 * 256;
+    ensure_pool(c, pool);
+    // sample-record budget: chunks of passes, each < 2^31 records
+    const size_t rec_budget = (size_t)6 << 30;
+    uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(passes, rec_budget / (16 * (size_t)M)));
+    chunk = (uint32_t)std::min<uint64_t>(chunk, ((uint64_t)1 << 31) / M);
+    c.rec.ensure(16 * (size_t)chunk * M);
+    c.counters.ensure(sizeof(Counters));
+    c.pixels.upload(pixels);
+    c.blocks.upload(blocks);
+    const size_t film_elems = 4 * (size_t)(W + 2 * B) * (H + 2 * B);
+    float *film = nullptr;
+    if (rd.output_on_device) {
+        film = rgbw_out;
+    } else {
+        c.film.ensure(film_elems * sizeof(float));
+        film = c.film.as<float>();
+        HIP_TRY(hipMemsetAsync(film, 0, film_elems * sizeof(float), c.stream));
+    }
+    if (!c.pinned) {
+        HIP_TRY(hipHostMalloc((void **)&c.pinned, kRing * 32, hipHostMallocDefault));
+        c.ring.resize(kRing);
+        for (auto &e : c.ring) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    Counters *C = c.counters.as<Counters>();
+    ShadowQueue sq{c.sq[0].as<float4>(), c.sq[1].as<float4>(), c.sq[2].as<float4>()};
+    PathQueue Q[2] = {queue_of(c, 0), queue_of(c, 1)};
+    c.cancel = 0;
+    c.progress = 0.0f;
+    const uint64_t total_all = (uint64_t)passes * M;
+    uint64_t done_before = 0, rays_c = 0, rays_s = 0, invalid = 0, iters = 0;
+    Timers tm;
+    struct Span {
+        hipEvent_t a, b;
+        int kind;
+    };
+    std::vector<Span> spans;
+    const bool timing = false;
+    bool cancelled = false;
+    for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
+        uint32_t np = std::min(chunk, passes - p0);
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed};
+        HIP_TRY(hipMemsetAsync(C, 0, sizeof(Counters), c.stream));
+        for (uint64_t it = 0;; ++it) {
+            int in = (int)(it & 1), out = in ^ 1, sh = (int)(it & 1);
+            HIP_TRY(launch_shade(S, Q[in], Q[out], sq, C, in, sh, wd, c.rec.as<float4>(), pool, c.stream));
+            HIP_TRY(launch_extend(S, Q[out], C, out, in, sh ^ 1, pool, c.stack, c.stream));
+            HIP_TRY(launch_shadow(S, sq, C, sh, c.rec.as<float4>(), pool, c.stack, c.stream));
+            int slot = (int)(it % kRing);
+            // snapshot {qcount[0..1], shadow_count[0..1], next_work}
+            HIP_TRY(hipMemcpyAsync(c.pinned + 8 * slot, C, 32, hipMemcpyDeviceToHost, c.stream));
+            HIP_TRY(hipEventRecord(c.ring[slot], c.stream));
+            ++iters;
+            if (it >= (uint64_t)kLookahead) {
+                uint64_t chk = it - kLookahead;
+                int cs = (int)(chk % kRing);
+                HIP_TRY(hipEventSynchronize(c.ring[cs]));
+                const uint32_t *snap = c.pinned + 8 * cs;
+                int chk_out = (int)((chk & 1) ^ 1);
+                uint64_t nw;
+                std::memcpy(&nw, snap + 4, 8);
+                c.progress = (float)std::min(1.0, (double)(done_before + std::min<uint64_t>(nw, wd.total)) / (double)total_all);
+                if (snap[chk_out] == 0 && nw >= wd.total) break;
+                if (c.cancel.load()) {
+                    cancelled = true;
+                    break;
+                }
+            }
+        }
+        if (cancelled) break;
+        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 16)),
+                     c.blocks.as<int4>(), rd.seed};
+        HIP_TRY(launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream));
+        Counters hc;
+        HIP_TRY(hipMemcpyAsync(&hc, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        rays_c += hc.rays_closest;
+        rays_s += hc.rays_shadow;
+        invalid += hc.invalid;
+        done_before += wd.total;
+    }
+    (void)timing;
+    (void)spans;
+    if (!rd.output_on_device && !cancelled) {
+        std::vector<float> hf(film_elems);
+        HIP_TRY(hipMemcpy(hf.data(), film, film_elems * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < film_elems; ++i) rgbw_out[i] += hf[i];
+    }
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    c.progress = 1.0f;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->samples = done_before;
+        stats->invalid_samples = invalid;
+        stats->rays_closest = rays_c;
+        stats->rays_shadow = rays_s;
+        stats->iterations = iters;
+        stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
+    return NORI_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char *nori_gpu_last_error(void) { return g_last_error.c_str(); }
+int nori_gpu_abi_version(void) { return NORI_GPU_ABI_VERSION; }
+
+int nori_scene_load_xml(const char *path, int width, int height, int spp, nori_scene **out) {
+    return guarded([&] {
+        if (!path || !out) return fail(NORI_ERR_INVALID, "null argument");
+        auto *s = new nori_scene;
+        s->hs.reset(load_scene_xml(path, width, height, spp));
+        *out = s;
+        return NORI_OK;
+    });
+}
+const nori_scene_desc *nori_scene_get_desc(const nori_scene *s) { return s ? &s->hs->desc : nullptr; }
+void nori_scene_free(nori_scene *s) { delete s; }
+
+int nori_film_border(const nori_scene_desc *d) { return d ? film_border(d->camera) : NORI_ERR_INVALID; }
+int nori_filter_table(const nori_scene_desc *d, float *table) {
+    if (!d || !table) return fail(NORI_ERR_INVALID, "null argument");
+    filter_table(d->camera, table);
+    return NORI_OK;
+}
+int nori_film_develop(const nori_scene_desc *d, const float *rgbw, float *rgb) {
+    if (!d || !rgbw || !rgb) return fail(NORI_ERR_INVALID, "null argument");
+    int W = d->camera.width, H = d->camera.height, B = film_border(d->camera), FW = W + 2 * B;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const float *c = rgbw + 4 * ((size_t)(y + B) * FW + (x + B));
+            float *o = rgb + 3 * ((size_t)y * W + x);
+            for (int k = 0; k < 3; ++k) o[k] = c[3] != 0 ? c[k] / c[3] : 0.0f;  // color.h:113-118
+        }
+    return NORI_OK;
+}
+
+int nori_gpu_device_count(int *count) {
+    return guarded([&] {
+        if (!count) return fail(NORI_ERR_INVALID, "null argument");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        *count = e == hipSuccess ? n : 0;
+        return NORI_OK;
+    });
+}
+
+int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
+    return guarded([&] {
+        if (!d || !out) return fail(NORI_ERR_INVALID, "null argument");
+        if (d->abi_version != NORI_GPU_ABI_VERSION) return fail(NORI_ERR_INVALID, "scene desc ABI version mismatch");
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(NORI_ERR_HIP, "no HIP device available");
+        if (device < 0 || device >= n) return fail(NORI_ERR_INVALID, "device index out of range");
+        HIP_TRY(hipSetDevice(device));
+        std::unique_ptr<nori_gpu_ctx> c(new nori_gpu_ctx);
+        c->device = device;
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        upload_scene(*c, *d);
+        *out = c.release();
+        return NORI_OK;
+    });
+}
+
+int nori_gpu_render(nori_gpu_ctx *c, const nori_gpu_render_desc *rd, float *rgbw_out, nori_gpu_stats *stats) {
+    return guarded([&] {
+        if (!c || !rd || !rgbw_out) return fail(NORI_ERR_INVALID, "null argument");
+        if (rd->num_blocks && !rd->block_ids) return fail(NORI_ERR_INVALID, "block_ids is null");
+        return render(*c, *rd, rgbw_out, stats);
+    });
+}
+
+int nori_gpu_trace(nori_gpu_ctx *c, const float *rays, uint32_t n, int any_hit, nori_gpu_hit *hits) {
+    return guarded([&] {
+        if (!c || !rays || !hits) return fail(NORI_ERR_INVALID, "null argument");
+        if (n == 0) return NORI_OK;
+        HIP_TRY(hipSetDevice(c->device));
+        DevBuf r, h;
+        r.ensure(32 * (size_t)n);
+        h.ensure(16 * (size_t)n);
+        HIP_TRY(hipMemcpy(r.p, rays, 32 * (size_t)n, hipMemcpyHostToDevice));
+        HIP_TRY(launch_trace(c->S, r.as<float4>(), n, any_hit, h.as<float4>(), c->stack, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(hits, h.p, 16 * (size_t)n, hipMemcpyDeviceToHost));
+        return NORI_OK;
+    });
+}
+
+int nori_gpu_cancel(nori_gpu_ctx *c) {
+    if (!c) return fail(NORI_ERR_INVALID, "null argument");
+    c->cancel = 1;
+    return NORI_OK;
+}
+float nori_gpu_progress(const nori_gpu_ctx *c) { return c ? c->progress.load() : 0.0f; }
+void nori_gpu_destroy(nori_gpu_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    delete c;
+}
+
+}  // extern "C"

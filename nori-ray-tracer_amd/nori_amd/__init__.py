@@ -1,0 +1,258 @@
+"""nori_amd -- MI355X wavefront path tracer behind Nori's scene/plugin API.
+
+Host-side mirror of the reference's render entry points:
+
+* :func:`load_scene` -- ``loadFromXML`` + ``Scene::activate`` (parser.cpp:28,
+  scene.cpp:43); the XML `type` names, properties and defaults are Nori's.
+* :class:`GpuRenderer` -- one HIP context per device (``nori_gpu_create``);
+  ``render`` replaces ``RenderThread::renderScene``'s pass loop
+  (render.cpp:173-250) and returns the RGBW image block with its filter
+  border (``ImageBlock``, block.h:48).
+* :class:`RenderThread` -- ``renderScene(xml)`` writing ``<stem>.exr`` like
+  render.cpp:158-261, with ``getProgress``/``stopRendering``.
+
+All compute goes through ``lib/libnori_gpu.so`` (C ABI, include/nori_gpu.h);
+there is no CPU fallback: without the library or a GPU the calls raise.
+"""
+import ctypes as C
+import os
+import threading
+import time
+
+import numpy as np
+
+from . import _abi
+from ._abi import NoriError, check, lib  # noqa: F401
+
+__all__ = ["load_scene", "Scene", "GpuRenderer", "RenderThread", "NoriError", "device_count",
+           "develop", "write_exr"]
+
+
+def _fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Scene:
+    """A loaded, flattened scene (owner of the nori_scene handle)."""
+
+    def __init__(self, handle, path):
+        self._h = C.c_void_p(handle)
+        self.path = path
+        self.desc_ptr = lib().nori_scene_get_desc(self._h)
+        self.desc = self.desc_ptr.contents
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _abi._lib is not None:
+            _abi._lib.nori_scene_free(h)
+            self._h = None
+
+    # convenience views
+    @property
+    def width(self):
+        return self.desc.camera.width
+
+    @property
+    def height(self):
+        return self.desc.camera.height
+
+    @property
+    def spp(self):
+        return self.desc.sample_count
+
+    @property
+    def border(self):
+        return lib().nori_film_border(self.desc_ptr)
+
+    @property
+    def integrator(self):
+        return _abi.INTEGRATOR_NAMES[self.desc.integrator]
+
+    def film_shape(self):
+        b = self.border
+        return (self.height + 2 * b, self.width + 2 * b, 4)
+
+    def positions(self):
+        n = self.desc.num_vertices
+        return np.ctypeslib.as_array(self.desc.positions, shape=(n, 3)).copy()
+
+    def indices(self):
+        n = self.desc.num_triangles
+        return np.ctypeslib.as_array(self.desc.indices, shape=(n, 3)).copy()
+
+    def shapes(self):
+        return [self.desc.shapes[i] for i in range(self.desc.num_shapes)]
+
+    def bsdfs(self):
+        return [self.desc.bsdfs[i] for i in range(self.desc.num_bsdfs)]
+
+    def emitters(self):
+        return [self.desc.emitters[i] for i in range(self.desc.num_emitters)]
+
+    def filter_table(self):
+        t = np.zeros(_abi.FILTER_RESOLUTION + 1, np.float32)
+        check(lib().nori_filter_table(self.desc_ptr, _fptr(t)))
+        return t
+
+    def num_blocks(self):
+        bs = _abi.BLOCK_SIZE
+        return ((self.width + bs - 1) // bs) * ((self.height + bs - 1) // bs)
+
+
+def load_scene(path, width=0, height=0, spp=0):
+    """Parse a Nori XML scene; width/height/spp > 0 override the XML values."""
+    h = C.c_void_p()
+    check(lib().nori_scene_load_xml(os.fsencode(path), int(width), int(height), int(spp), C.byref(h)))
+    return Scene(h.value, path)
+
+
+def device_count():
+    n = C.c_int(0)
+    check(lib().nori_gpu_device_count(C.byref(n)))
+    return n.value
+
+
+def develop(scene, rgbw):
+    """ImageBlock::toBitmap (block.cpp:76-82): RGB / W without the border."""
+    rgbw = np.ascontiguousarray(rgbw, dtype=np.float32)
+    if rgbw.shape != scene.film_shape():
+        raise ValueError(f"film shape {rgbw.shape} != {scene.film_shape()}")
+    out = np.zeros((scene.height, scene.width, 3), np.float32)
+    check(lib().nori_film_develop(scene.desc_ptr, _fptr(rgbw), _fptr(out)))
+    return out
+
+
+def write_exr(path, rgb):
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    check(lib().nori_write_exr(os.fsencode(path), _fptr(rgb), rgb.shape[1], rgb.shape[0]))
+
+
+class GpuRenderer:
+    """HIP context holding one scene on one device (nori_gpu_create)."""
+
+    def __init__(self, scene, device=0):
+        self.scene = scene  # keeps the host arrays alive
+        h = C.c_void_p()
+        check(lib().nori_gpu_create(scene.desc_ptr, int(device), C.byref(h)))
+        self._h = h
+        self.device = device
+        self.last_stats = None
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().nori_gpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def render(self, passes=None, pass_begin=0, blocks=None, seed=0, out=None, path_pool=0,
+               device_ptr=None):
+        """Render passes [pass_begin, pass_begin+passes) of `blocks` (all if None).
+
+        Returns the RGBW film (H+2b, W+2b, 4) as float32, accumulated into
+        `out` when given.  With `device_ptr` (an int device address, e.g. a
+        torch tensor's data_ptr()) the film is accumulated on the GPU instead.
+        """
+        rd = _abi.RenderDesc()
+        rd.pass_begin = int(pass_begin)
+        rd.pass_count = int(self.scene.spp if passes is None else passes)
+        ids = None
+        if blocks is not None:
+            ids = np.ascontiguousarray(np.asarray(blocks, dtype=np.uint32))
+            rd.num_blocks = ids.size
+            rd.block_ids = ids.ctypes.data_as(C.POINTER(C.c_uint32))
+        rd.seed = int(seed)
+        rd.path_pool = int(path_pool)
+        st = _abi.Stats()
+        if device_ptr is not None:
+            rd.output_on_device = 1
+            check(lib().nori_gpu_render(self._h, C.byref(rd), C.c_void_p(int(device_ptr)), C.byref(st)))
+            self.last_stats = st.as_dict()
+            return None
+        if out is None:
+            out = np.zeros(self.scene.film_shape(), np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.shape == self.scene.film_shape()
+        check(lib().nori_gpu_render(self._h, C.byref(rd), out.ctypes.data_as(C.c_void_p), C.byref(st)))
+        self.last_stats = st.as_dict()
+        return out
+
+    def trace(self, rays, any_hit=False):
+        """Scene::rayIntersect on a batch: rays (n, 8) = o.xyz, mint, d.xyz, maxt."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        n = rays.shape[0]
+        hits = (_abi.Hit * n)()
+        check(lib().nori_gpu_trace(self._h, _fptr(rays), n, int(bool(any_hit)), hits))
+        a = np.frombuffer(hits, dtype=np.dtype([("t", "<f4"), ("prim", "<i4"), ("u", "<f4"), ("v", "<f4")]))
+        return a.copy()
+
+    def cancel(self):
+        check(lib().nori_gpu_cancel(self._h))
+
+    def progress(self):
+        return lib().nori_gpu_progress(self._h)
+
+
+class RenderThread:
+    """Mirror of nori::RenderThread (render.h:29-52) over the GPU path."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self._thread = None
+        self._renderer = None
+        self._status = 0  # 0 idle, 1 rendering, 2 stop requested, 3 done
+        self.error = None
+        self.image = None
+
+    def renderScene(self, filename, width=0, height=0, spp=0):
+        scene = load_scene(filename, width, height, spp)
+        stem = os.path.splitext(filename)[0]
+
+        def run():
+            try:
+                self._renderer = GpuRenderer(scene, self.device)
+                t0 = time.time()
+                print("Rendering .. ", end="", flush=True)
+                film = self._renderer.render()
+                print(f"done. (took {1e3 * (time.time() - t0):.1f}ms)")
+                self.image = develop(scene, film)
+                write_exr(stem + ".exr", self.image)
+            except NoriError as e:
+                self.error = e
+            finally:
+                if self._renderer is not None:
+                    self._renderer.close()
+                self._status = 3
+
+        self._status = 1
+        self._thread = threading.Thread(target=run)
+        self._thread.start()
+
+    def isBusy(self):
+        if self._status == 3:
+            self._thread.join()
+            self._status = 0
+        return self._status != 0
+
+    def isRenderingDone(self):
+        return self._status == 3
+
+    def getProgress(self):
+        r = self._renderer
+        return r.progress() if (r is not None and self._status in (1, 2)) else 1.0
+
+    def stopRendering(self):
+        if self._status in (1, 2) and self._renderer is not None:
+            self._status = 2
+            self._renderer.cancel()
+            self._thread.join()
+            self._status = 0
