@@ -182,6 +182,7 @@ typedef struct nori_gpu_render_desc {
     uint64_t seed;                /* stream seed mixed into every sample id     */
     int32_t output_on_device;     /* rgbw_out is a device pointer on ctx device */
     uint32_t path_pool;           /* paths in flight (0 = default)              */
+    int32_t timing;               /* nonzero: HIP events around every launch    */
 } nori_gpu_render_desc;
 
 typedef struct nori_gpu_stats {
@@ -189,9 +190,12 @@ typedef struct nori_gpu_stats {
     uint64_t invalid_samples;     /* NaN/Inf/negative radiance, dropped (block.cpp:94-98) */
     uint64_t rays_closest;        /* extension rays traced                      */
     uint64_t rays_shadow;         /* shadow rays traced                         */
-    uint64_t iterations;          /* wavefront iterations                       */
+    uint64_t iterations;          /* wavefront iterations (= extend launches)   */
+    uint64_t scene_bytes;         /* BVH nodes + primitive records in HBM       */
+    uint32_t bvh_nodes, bvh_depth;
     double ms_total;              /* render wall time (host timer)              */
-    double ms_extend, ms_shadow, ms_shade, ms_splat;  /* HIP-event kernel time  */
+    /* with desc.timing: summed HIP-event time of each kernel, on the launch stream */
+    double ms_extend, ms_shadow, ms_shade, ms_splat;
 } nori_gpu_stats;
 
 typedef struct nori_gpu_hit {

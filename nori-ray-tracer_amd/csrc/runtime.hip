@@ -458,7 +458,18 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         int kind;
     };
     std::vector<Span> spans;
-    const bool timing = false;
+    const bool timing = rd.timing != 0;
+    auto timed = [&](int kind, auto &&launch) {
+        if (!timing) {
+            HIP_TRY(launch());
+            return;
+        }
+        Span s{tm.get(), tm.get(), kind};
+        HIP_TRY(hipEventRecord(s.a, c.stream));
+        HIP_TRY(launch());
+        HIP_TRY(hipEventRecord(s.b, c.stream));
+        spans.push_back(s);
+    };
     bool cancelled = false;
     for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
         uint32_t np = std::min(chunk, passes - p0);
@@ -466,9 +477,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipMemsetAsync(C, 0, sizeof(Counters), c.stream));
         for (uint64_t it = 0;; ++it) {
             int in = (int)(it & 1), out = in ^ 1, sh = (int)(it & 1);
-            HIP_TRY(launch_shade(S, Q[in], Q[out], sq, C, in, sh, wd, c.rec.as<float4>(), pool, c.stream));
-            HIP_TRY(launch_extend(S, Q[out], C, out, in, sh ^ 1, pool, c.stack, c.stream));
-            HIP_TRY(launch_shadow(S, sq, C, sh, c.rec.as<float4>(), pool, c.stack, c.stream));
+            timed(2, [&] { return launch_shade(S, Q[in], Q[out], sq, C, in, sh, wd, c.rec.as<float4>(), pool, c.stream); });
+            timed(0, [&] { return launch_extend(S, Q[out], C, out, in, sh ^ 1, pool, c.stack, c.stream); });
+            timed(1, [&] { return launch_shadow(S, sq, C, sh, c.rec.as<float4>(), pool, c.stack, c.stream); });
             int slot = (int)(it % kRing);
             // snapshot {qcount[0..1], shadow_count[0..1], next_work}
             HIP_TRY(hipMemcpyAsync(c.pinned + 8 * slot, C, 32, hipMemcpyDeviceToHost, c.stream));
@@ -493,7 +504,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         if (cancelled) break;
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 16)),
                      c.blocks.as<int4>(), rd.seed};
-        HIP_TRY(launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream));
+        timed(3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream); });
         Counters hc;
         HIP_TRY(hipMemcpyAsync(&hc, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
         HIP_TRY(hipStreamSynchronize(c.stream));
@@ -502,8 +513,15 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         invalid += hc.invalid;
         done_before += wd.total;
     }
-    (void)timing;
-    (void)spans;
+    double kms[4] = {0, 0, 0, 0};
+    if (timing) {
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        for (const Span &s : spans) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, s.a, s.b));
+            kms[s.kind] += ms;
+        }
+    }
     if (!rd.output_on_device && !cancelled) {
         std::vector<float> hf(film_elems);
         HIP_TRY(hipMemcpy(hf.data(), film, film_elems * sizeof(float), hipMemcpyDeviceToHost));
@@ -518,7 +536,14 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         stats->rays_closest = rays_c;
         stats->rays_shadow = rays_s;
         stats->iterations = iters;
+        stats->scene_bytes = c.scene_bytes;
+        stats->bvh_nodes = c.bvh_nodes;
+        stats->bvh_depth = c.bvh_depth;
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->ms_extend = kms[0];
+        stats->ms_shadow = kms[1];
+        stats->ms_shade = kms[2];
+        stats->ms_splat = kms[3];
     }
     if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
     return NORI_OK;

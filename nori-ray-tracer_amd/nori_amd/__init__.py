@@ -156,7 +156,7 @@ class GpuRenderer:
         self.close()
 
     def render(self, passes=None, pass_begin=0, blocks=None, seed=0, out=None, path_pool=0,
-               device_ptr=None):
+               device_ptr=None, timing=False):
         """Render passes [pass_begin, pass_begin+passes) of `blocks` (all if None).
 
         Returns the RGBW film (H+2b, W+2b, 4) as float32, accumulated into
@@ -173,6 +173,7 @@ class GpuRenderer:
             rd.block_ids = ids.ctypes.data_as(C.POINTER(C.c_uint32))
         rd.seed = int(seed)
         rd.path_pool = int(path_pool)
+        rd.timing = int(bool(timing))
         st = _abi.Stats()
         if device_ptr is not None:
             rd.output_on_device = 1

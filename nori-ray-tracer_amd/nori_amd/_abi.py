@@ -75,12 +75,13 @@ class SceneDesc(C.Structure):
 class RenderDesc(C.Structure):
     _fields_ = [("pass_begin", C.c_uint32), ("pass_count", C.c_uint32), ("num_blocks", C.c_uint32),
                 ("block_ids", C.POINTER(C.c_uint32)), ("seed", C.c_uint64),
-                ("output_on_device", C.c_int32), ("path_pool", C.c_uint32)]
+                ("output_on_device", C.c_int32), ("path_pool", C.c_uint32), ("timing", C.c_int32)]
 
 
 class Stats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("invalid_samples", C.c_uint64), ("rays_closest", C.c_uint64),
-                ("rays_shadow", C.c_uint64), ("iterations", C.c_uint64), ("ms_total", C.c_double),
+                ("rays_shadow", C.c_uint64), ("iterations", C.c_uint64), ("scene_bytes", C.c_uint64),
+                ("bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32), ("ms_total", C.c_double),
                 ("ms_extend", C.c_double), ("ms_shadow", C.c_double), ("ms_shade", C.c_double),
                 ("ms_splat", C.c_double)]
 
