@@ -189,9 +189,11 @@ def main():
                          "bytes_per_launch": bytes_total / launches,
                          "avg_launch_ms": ts["ms_extend"] / launches, "launches": launches},
             "kernel_ms": {"extend": ts["ms_extend"], "shadow": ts["ms_shadow"], "shade": ts["ms_shade"],
-                          "splat": ts["ms_splat"], "wall": ts["ms_total"]},
+                          "splat": ts["ms_splat"], "finish": ts["ms_finish"], "wall": ts["ms_total"]},
             "rays_per_sample": {"closest": ts["rays_closest"] / samples_per_step,
-                                "shadow": ts["rays_shadow"] / samples_per_step},
+                                "shadow": ts["rays_shadow"] / samples_per_step,
+                                "finisher": ts["rays_finish"] / samples_per_step},
+            "wavefront_iterations": ts["iterations"],
         }
         if world == 1 and not args.no_parity:
             out["parity"] = parity_check()

@@ -188,14 +188,15 @@ typedef struct nori_gpu_render_desc {
 typedef struct nori_gpu_stats {
     uint64_t samples;             /* camera samples completed                   */
     uint64_t invalid_samples;     /* NaN/Inf/negative radiance, dropped (block.cpp:94-98) */
-    uint64_t rays_closest;        /* extension rays traced                      */
-    uint64_t rays_shadow;         /* shadow rays traced                         */
+    uint64_t rays_closest;        /* extension rays traced by k_extend          */
+    uint64_t rays_shadow;         /* shadow rays traced by k_shadow             */
+    uint64_t rays_finish;         /* rays traced inside the tail finisher       */
     uint64_t iterations;          /* wavefront iterations (= extend launches)   */
     uint64_t scene_bytes;         /* BVH nodes + primitive records in HBM       */
     uint32_t bvh_nodes, bvh_depth;
     double ms_total;              /* render wall time (host timer)              */
     /* with desc.timing: summed HIP-event time of each kernel, on the launch stream */
-    double ms_extend, ms_shadow, ms_shade, ms_splat;
+    double ms_extend, ms_shadow, ms_shade, ms_splat, ms_finish;
 } nori_gpu_stats;
 
 typedef struct nori_gpu_hit {

@@ -49,6 +49,8 @@ struct DevScene {
     const float *cdf;
     uint32_t num_emitters;
     uint32_t num_nodes;
+    uint32_t num_prims;
+    float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;
     float invW, invH;
     float s2c[16];
@@ -79,22 +81,44 @@ struct ShadowQueue {
     float4 *payload;
 };
 
-// Work decomposition: work id w in [0, total) -> pass w / M, list entry w % M.
+// Segmented queues: shade work-group b owns queue entries [b*kSeg, (b+1)*kSeg)
+// of the path queues and of the shadow queue; counts are per segment, so no
+// global atomics are needed to compact.  Work ids reach a segment through a
+// static stream of 256-id chunks (consecutive ids = adjacent pixels of one
+// 32x32 block, so a segment traces coherent camera rays).
+constexpr uint32_t kSeg = 256;
 struct WorkDesc {
-    uint64_t total;
+    uint64_t total;          // work ids in this chunk of passes
     uint32_t M;              // pixels in the selected blocks
     uint32_t pass_begin;     // absolute pass of work id 0
     const uint32_t *pixels;  // M entries, y*W + x, block-major
     uint64_t seed;
+    uint32_t G;              // segments
+    uint32_t *done_flag;     // host-mapped: set when the last segment exhausts its stream
+};
+// Round j hands segment b the chunk (b + j*kRotate) mod G of that round, so a
+// segment sees a different part of the image every round (path lengths vary
+// strongly across the image; a fixed pixel set per segment drains unevenly).
+constexpr uint32_t kRotate = 1031;  // odd: coprime with the power-of-two G
+NHD uint64_t stream_work(const WorkDesc &wd, uint32_t b, uint32_t p) {
+    uint64_t j = p / kSeg;
+    uint64_t col = (b + j * kRotate) % wd.G;
+    return (j * wd.G + col) * kSeg + (p % kSeg);
+}
+
+struct SegState {
+    uint32_t *cnt[2];   // paths per segment (ping-pong)
+    uint32_t *shcnt;    // shadow rays per segment
+    uint32_t *cursor;   // work-stream position per segment
+    uint4 *stats;       // per segment: extension rays, shadow rays, samples started, finisher rays
 };
 
-// Device counters (one 256-byte line, zeroed per render).
+// Device counters, each on its own 128-byte line.
 struct Counters {
-    uint32_t qcount[2];           // path queue sizes (ping-pong)
-    uint32_t shadow_count[2];     // shadow queue size (ping-pong by iteration parity)
-    unsigned long long next_work; // work ids handed out
-    unsigned long long rays_closest, rays_shadow, invalid;
-    unsigned long long pad[25];
+    uint32_t exhausted;            // segments whose work stream is used up
+    uint32_t pad0[31];
+    unsigned long long invalid;    // dropped samples (splat)
+    unsigned long long pad1[15];
 };
 
 }  // namespace nori

@@ -23,12 +23,14 @@ struct SplatDesc {
 hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int any_hit, float4 *hits, int stack,
                         hipStream_t st);
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                        Counters *C, int in_sel, int sh_sel, const WorkDesc &wd, float4 *rec, uint32_t pool,
+                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                         hipStream_t st);
-hipError_t launch_extend(const DevScene &S, const PathQueue &q, Counters *C, int q_sel, int reset_q, int reset_sh,
-                         uint32_t pool, int stack, hipStream_t st);
-hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, Counters *C, int sh_sel, float4 *rec,
-                         uint32_t pool, int stack, hipStream_t st);
+hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
+                         hipStream_t st);
+hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
+                         int stack, hipStream_t st);
+hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
+                         uint32_t G, int stack, hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 

@@ -4,12 +4,15 @@
 //   k_shade   : per path: surface hit -> emission, next-event estimation
 //               (light sample + shadow ray), Russian roulette, BSDF sample,
 //               or regeneration of a finished path slot with a new camera
-//               sample.  Output paths and shadow rays are compacted with a
-//               64-lane ballot + mbcnt prefix and one atomic per wave.
+//               sample.  Work-group b owns queue segment b; survivors and
+//               shadow rays are compacted inside the segment with 64-lane
+//               ballots + an LDS prefix over the 4 waves (no global atomics).
 //   k_extend  : closest-hit BVH traversal of the compacted path queue.
 //   k_shadow  : any-hit traversal; unoccluded rays add their payload to the
 //               sample record (the reference's `color +=`, path_mis.cpp:48-60).
-// After the queue drains, k_splat filters every sample into the RGBW film.
+// Once every segment's work stream is used up, k_finish runs the remaining
+// paths to completion one thread per path (no per-bounce launches for the
+// Russian-roulette tail), then k_splat filters every sample into the film.
 //
 // This replaces render.cpp:194-233 (pass loop + tbb::parallel_for),
 // renderBlock (render.cpp:80-133), PathMisIntegrator::Li (path_mis.cpp:17-101),
@@ -26,20 +29,6 @@ ND uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_m
 ND uint32_t rank_in(uint64_t mask) {  // set lanes of `mask` below this lane
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
-// Reserve `popc(mask)` slots on a device counter with one atomic per wave.
-// Must be called by all 64 lanes of the wave (uniform control flow).
-ND uint32_t wave_reserve(uint32_t *counter, uint64_t mask) {
-    uint32_t base = 0;
-    if (lane_id() == 0 && mask) base = atomicAdd(counter, (uint32_t)__popcll(mask));
-    return __shfl(base, 0);
-}
-ND unsigned long long wave_reserve64(unsigned long long *counter, uint64_t mask) {
-    unsigned long long base = 0;
-    if (lane_id() == 0 && mask) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
-    uint32_t lo = __shfl((uint32_t)base, 0), hi = __shfl((uint32_t)(base >> 32), 0);
-    return ((unsigned long long)hi << 32) | lo;
-}
-
 // ------------------------------------------------------------------ traversal
 struct TRay {
     V3 o, d, rcp;
@@ -100,6 +89,37 @@ ND bool sphere_hit(const float4 &a, const float4 &b, const TRay &r, float &t) {
     return false;
 }
 
+// Branch-free forms of the two tests for the wave-uniform scan: every lane
+// evaluates the whole test and the acceptance predicate is the conjunction of
+// the reference's early-out conditions, so the accepted (t, u, v) are the
+// same values; lanes of a wave never split inside a primitive test.
+ND bool tri_hit_nb(const float4 &a, const float4 &b, const float4 &c, const TRay &r, float &t, float &u, float &v) {
+    V3 v0 = ld3(a), e1 = ld3(b), e2 = ld3(c);
+    V3 pvec = cross(r.d, e2);
+    float det = dot(e1, pvec);
+    float inv_det = 1.0f / det;
+    V3 tvec = r.o - v0;
+    u = dot(tvec, pvec) * inv_det;
+    V3 qvec = cross(tvec, e1);
+    v = dot(r.d, qvec) * inv_det;
+    t = dot(e2, qvec) * inv_det;
+    return !(det > -1e-8f && det < 1e-8f) && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) &&
+           t >= r.mint && t <= r.maxt;
+}
+ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t) {
+    V3 oc = r.o - ld3(a);
+    float rad = b.x;
+    float A = dot(r.d, r.d);
+    float B = 2.0f * dot(oc, r.d);
+    float C = dot(oc, oc) - rad * rad;
+    float disc = (B * B - 4 * A * C);
+    float delta = sqrtf(B * B - 4 * A * C);
+    float t1 = (-B - delta) / (2 * A), t2 = (-B + delta) / (2 * A);
+    bool h1 = r.mint <= t1 && t1 <= r.maxt, h2 = r.mint <= t2 && t2 <= r.maxt;
+    t = h1 ? t1 : t2;
+    return (disc > 0) && (h1 || h2);
+}
+
 // BVH::rayIntersect (bvh.cpp:404-462): adaptive epsilon, closest or any hit.
 // Near child first; the short stack lives in LDS, one column per lane.
 template <int STACK, bool ANY>
@@ -108,8 +128,45 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     tb = INF_F;
     pb = 0xFFFFFFFFu;
     ub = vb = 0.0f;
-    if (r.maxt < r.mint) return false;
     r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    if constexpr (STACK == 0) {
+        // Small scenes: wave-uniform scan of the primitive list.  Every lane
+        // tests every primitive in the same order, so the records arrive
+        // through scalar loads and no lane diverges; the result is the
+        // closest hit (ties: last primitive wins, as with the reference's
+        // `t <= maxt` update, mesh.cpp:119).  The root box test of
+        // bvh.cpp:420 is kept so rays missing the scene never report hits.
+        const float4 rmn = make_float4(S.root_min[0], S.root_min[1], S.root_min[2], 0.f);
+        const float4 rmx = make_float4(S.root_max[0], S.root_max[1], S.root_max[2], 0.f);
+        float tn;
+        bool live = !(r.maxt < r.mint) && box_test(rmn, rmx, r, tn);
+        bool found = false;
+        const uint32_t n = S.num_prims;
+        auto test = [&](uint32_t i) {
+            const float4 *p = S.prims + 3 * (size_t)i;
+            float4 p0 = p[0], p1 = p[1], p2 = p[2];
+            float t = 0, u = 0, v = 0;
+            bool tri = __float_as_uint(p1.w) == 0u;
+            bool h = tri ? tri_hit_nb(p0, p1, p2, r, t, u, v) : sphere_hit_nb(p0, p1, r, t);
+            if (h && live) {
+                found = true;
+                if (!ANY) {
+                    r.maxt = tb = t;
+                    ub = tri ? u : 0.0f;
+                    vb = tri ? v : 0.0f;
+                    pb = __float_as_uint(p0.w);
+                }
+            }
+        };
+        if constexpr (ANY) {
+            for (uint32_t i = 0; i < n && !__all(found || !live); ++i) test(i);
+        } else {
+#pragma unroll 2
+            for (uint32_t i = 0; i < n; ++i) test(i);
+        }
+        return found;
+    }
+    if (r.maxt < r.mint) return false;
     uint32_t ref = 0;
     int sp = 0;
     bool found = false;
@@ -165,7 +222,7 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
 
 template <int STACK, bool ANY>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 *rays, uint32_t n, float4 *hits) {
-    __shared__ uint32_t stk[STACK * kTraceBlock];
+    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
     uint32_t q = blockIdx.x * kTraceBlock + threadIdx.x;
     if (q >= n) return;
     float4 a = rays[2 * (size_t)q], b = rays[2 * (size_t)q + 1];
@@ -181,20 +238,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 
     else hits[q] = make_float4(t, __uint_as_float(p), u, v);
 }
 
-// Extension rays: closest hit of every queued path.  Thread 0 also clears the
-// counters the next shade launch appends to (placed here so that no extra
-// launch is needed: they were last read by the previous shade / shadow).
+// Extension rays: closest hit of every queued path (two blocks per segment).
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, Counters *C, int q_sel, int reset_q,
-                                                        int reset_sh) {
-    __shared__ uint32_t stk[STACK * kTraceBlock];
-    uint32_t q = blockIdx.x * kTraceBlock + threadIdx.x;
-    if (q == 0) {
-        C->qcount[reset_q] = 0;
-        C->shadow_count[reset_sh] = 0;
-    }
-    uint32_t n = C->qcount[q_sel];
-    if (q >= n) return;
+__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt) {
+    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    const uint32_t seg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
+    if (idx >= cnt[seg]) return;
+    const uint32_t q = seg * kSeg + idx;
     float4 a = pq.ray_o[q], b = pq.ray_d[q];
     TRay r;
     r.o = ld3(a);
@@ -209,12 +259,12 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq
 
 // Shadow rays: any hit; unoccluded -> record += payload.
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue sq, Counters *C, int sh_sel,
+__global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
                                                         float4 *rec) {
-    __shared__ uint32_t stk[STACK * kTraceBlock];
-    uint32_t q = blockIdx.x * kTraceBlock + threadIdx.x;
-    uint32_t n = C->shadow_count[sh_sel];
-    if (q >= n) return;
+    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    const uint32_t seg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
+    if (idx >= shcnt[seg]) return;
+    const uint32_t q = seg * kSeg + idx;
     float4 a = sq.ray_o[q], b = sq.ray_d[q];
     TRay r;
     r.o = ld3(a);
@@ -324,212 +374,331 @@ ND void camera_ray(const DevScene &S, float px, float py, V3 &o, V3 &d, float &m
 }
 
 // ------------------------------------------------------------------ shade + regenerate
-// INTEG: NORI_INTEGRATOR_PATH_MIS or NORI_INTEGRATOR_PATH_MATS.
+struct PathState {
+    V3 o, d;
+    float mint, maxt;
+    V3 beta;
+    float prev;  // BSDF pdf of the last bounce; -1: w_mats = 1 (camera ray or discrete lobe)
+    Pcg rng;
+    uint32_t work;
+};
+struct ShadowOut {
+    bool emit;
+    V3 o, d, contrib;
+    float maxt;
+    uint32_t work;
+};
+
+ND void load_path(const PathQueue &Q, uint32_t q, PathState &ps) {
+    float4 ro = Q.ray_o[q], rd = Q.ray_d[q], th = Q.thr[q];
+    uint4 rs = Q.rng[q];
+    ps.o = ld3(ro);
+    ps.d = ld3(rd);
+    ps.mint = ro.w;
+    ps.maxt = rd.w;
+    ps.beta = ld3(th);
+    ps.prev = th.w;
+    ps.rng.state = ((uint64_t)rs.y << 32) | rs.x;
+    ps.rng.inc = ((uint64_t)rs.w << 32) | rs.z;
+    ps.work = Q.work[q];
+}
+ND void store_path(const PathQueue &Q, uint32_t i, const PathState &ps) {
+    Q.ray_o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.mint);
+    Q.ray_d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, ps.maxt);
+    Q.thr[i] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, ps.prev);
+    Q.rng[i] = make_uint4((uint32_t)ps.rng.state, (uint32_t)(ps.rng.state >> 32), (uint32_t)ps.rng.inc,
+                          (uint32_t)(ps.rng.inc >> 32));
+    Q.work[i] = ps.work;
+}
+
+// One vertex of PathMisIntegrator::Li (path_mis.cpp:32-97) or
+// PathMatsIntegrator::Li (path_mats.cpp:26-57) given the closest hit of the
+// current ray.  Returns true if the path continues (ps holds the new ray).
+template <int INTEG>
+ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
+    so.emit = false;
+    uint32_t prim = __float_as_uint(h.y);
+    if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
+    SurfHit hs = surface(S, prim, h.x, h.z, h.w, ps.o, ps.d);
+    const DevShape &sh = S.shapes[hs.shape];
+    const DevBsdf &B = S.bsdfs[sh.bsdf];
+    if (sh.emitter >= 0) {  // emission (path_mis.cpp:35-39, path_mats.cpp:31-35)
+        const DevEmitter &E = S.emitters[sh.emitter];
+        V3 wi = normalize(hs.p - ps.o);
+        V3 Le = emitter_eval(E, hs.sh.n, wi);
+        V3 Ladd;
+        if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
+            float w = 1.0f;  // w_mats (path_mis.cpp:87-97)
+            if (ps.prev >= 0.0f) {
+                float pe = emitter_pdf(S, E, hs.sh.n, wi);
+                w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
+            }
+            Ladd = (ps.beta * w) * Le;
+        } else {
+            Ladd = ps.beta * Le;
+        }
+        float4 L = rec[ps.work];
+        rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, 0.0f);
+    }
+    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
+        float ul = next1D(ps.rng);
+        uint32_t N = S.num_emitters;
+        uint32_t li = (uint32_t)floorf((float)N * ul);
+        if (li > N - 1) li = N - 1;
+        const DevEmitter &E = S.emitters[li];
+        V2 s2 = next2D(ps.rng);
+        V3 lp, ln;
+        sample_surface(S, S.shapes[E.shape], s2, lp, ln);
+        V3 dv = lp - hs.p;
+        V3 wi = normalize(dv);
+        float pdf_em = emitter_pdf(S, E, ln, wi);
+        float att = dot(ln, -wi) / dot(dv, dv);
+        V3 Li = pdf_em > 0.0f ? (emitter_eval(E, ln, wi) * att) / pdf_em : V3{0, 0, 0};
+        Li = Li * (float)N;
+        BRec br;
+        br.wi = to_local(hs.sh, -ps.d);
+        br.wo = to_local(hs.sh, wi);
+        br.measure = kMeasureSolidAngle;
+        float theta = smax(0.0f, br.wo.z);
+        V3 f = bsdf_eval(B, br);
+        float pdf_mat = bsdf_pdf(B, br);
+        float w_ems = (pdf_mat + pdf_em) > 0.0f ? pdf_em / (pdf_mat + pdf_em) : pdf_em;
+        so.contrib = (((ps.beta * w_ems) * f) * theta) * Li;
+        so.emit = !is_zero(so.contrib);  // a zero contribution adds nothing (NaN still goes)
+        so.o = hs.p;
+        so.d = wi;
+        so.maxt = norm(dv) - kEps;
+        so.work = ps.work;
+    }
+    // Russian roulette on the red channel (path_mis.cpp:64-69)
+    float qrr = smin(ps.beta.x, 0.99f);
+    if (next1D(ps.rng) > qrr) return false;
+    ps.beta = ps.beta / qrr;
+    BRec br;
+    br.wi = to_local(hs.sh, -ps.d);
+    br.wo = V3{0, 0, 1};
+    br.measure = kMeasureUnknown;
+    V3 w = bsdf_sample(B, br, next2D(ps.rng));
+    if (is_zero(w)) return false;  // deviation D1: zero-weight samples end the path
+    ps.beta = ps.beta * w;
+    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
+        float pm = bsdf_pdf(B, br);
+        ps.prev = br.measure == kMeasureDiscrete ? -1.0f : pm;
+    }
+    ps.o = hs.p;
+    ps.d = to_world(hs.sh, br.wo);
+    ps.mint = kEps;
+    ps.maxt = INF_F;
+    return true;
+}
+
+// New camera sample for work id w (render.cpp:98-126 + independent.cpp).
+ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, PathState &ps, float4 *rec) {
+    uint32_t pass = w / wd.M, e = w - pass * wd.M;
+    uint32_t pix = wd.pixels[e];
+    uint32_t W = (uint32_t)S.W;
+    uint32_t y = pix / W, x = pix - y * W;
+    uint64_t sid = (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix;
+    wave_seed(ps.rng, wd.seed, sid);
+    V2 jit = next2D(ps.rng);
+    (void)next2D(ps.rng);  // apertureSample (render.cpp:99)
+    camera_ray(S, (float)x + jit.x, (float)y + jit.y, ps.o, ps.d, ps.mint, ps.maxt);
+    ps.beta = V3{1, 1, 1};
+    ps.prev = -1.0f;
+    ps.work = w;
+    rec[w] = make_float4(0, 0, 0, 0);
+}
+
 template <int INTEG>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathQueue in, PathQueue out, ShadowQueue sq,
-                                                       Counters *C, int in_sel, int sh_sel, WorkDesc wd,
-                                                       float4 *rec) {
-    const uint32_t q = blockIdx.x * kShadeBlock + threadIdx.x;
-    const uint32_t n_in = C->qcount[in_sel];
-
-    bool alive = false, shadow = false;
-    V3 no = {0, 0, 0}, nd = {0, 0, 1}, beta = {1, 1, 1};
-    float prev = -1.0f;
-    Pcg rng = {0, 1};
-    uint32_t work = 0, swork = 0;
-    V3 so = {0, 0, 0}, sdir = {0, 0, 1}, contrib = {0, 0, 0};
-    float smaxt = 0.0f;
-
-    if (q < n_in) {
-        float4 h = in.hit[q];
-        uint32_t prim = __float_as_uint(h.y);
-        work = in.work[q];
-        if (prim != 0xFFFFFFFFu) {
-            float4 ro = in.ray_o[q], rd = in.ray_d[q], th = in.thr[q];
-            uint4 rs = in.rng[q];
-            rng.state = ((uint64_t)rs.y << 32) | rs.x;
-            rng.inc = ((uint64_t)rs.w << 32) | rs.z;
-            V3 o = ld3(ro), d = ld3(rd);
-            beta = ld3(th);
-            prev = th.w;
-            SurfHit hs = surface(S, prim, h.x, h.z, h.w, o, d);
-            const DevShape &sh = S.shapes[hs.shape];
-            const DevBsdf &B = S.bsdfs[sh.bsdf];
-            V3 Ladd = {0, 0, 0};
-            bool add = false;
-            if (sh.emitter >= 0) {  // emission (path_mis.cpp:35-39, path_mats.cpp:31-35)
-                const DevEmitter &E = S.emitters[sh.emitter];
-                V3 wi = normalize(hs.p - o);
-                V3 Le = emitter_eval(E, hs.sh.n, wi);
-                if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
-                    float w = 1.0f;  // w_mats (path_mis.cpp:87-97)
-                    if (prev >= 0.0f) {
-                        float pe = emitter_pdf(S, E, hs.sh.n, wi);
-                        w = prev + pe > 0.f ? prev / (prev + pe) : prev;
-                    }
-                    Ladd = (beta * w) * Le;
-                } else {
-                    Ladd = beta * Le;
-                }
-                add = true;
-            }
-            if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
-                float ul = next1D(rng);
-                uint32_t N = S.num_emitters;
-                uint32_t li = (uint32_t)floorf((float)N * ul);
-                if (li > N - 1) li = N - 1;
-                const DevEmitter &E = S.emitters[li];
-                V2 s2 = next2D(rng);
-                V3 lp, ln;
-                sample_surface(S, S.shapes[E.shape], s2, lp, ln);
-                V3 dv = lp - hs.p;
-                V3 wi = normalize(dv);
-                float pdf_em = emitter_pdf(S, E, ln, wi);
-                float att = dot(ln, -wi) / dot(dv, dv);
-                V3 Li = pdf_em > 0.0f ? (emitter_eval(E, ln, wi) * att) / pdf_em : V3{0, 0, 0};
-                Li = Li * (float)N;
-                BRec br;
-                br.wi = to_local(hs.sh, -d);
-                br.wo = to_local(hs.sh, wi);
-                br.measure = kMeasureSolidAngle;
-                float theta = smax(0.0f, br.wo.z);
-                V3 f = bsdf_eval(B, br);
-                float pdf_mat = bsdf_pdf(B, br);
-                float w_ems = (pdf_mat + pdf_em) > 0.0f ? pdf_em / (pdf_mat + pdf_em) : pdf_em;
-                contrib = (((beta * w_ems) * f) * theta) * Li;
-                shadow = !is_zero(contrib);
-                swork = work;
-                so = hs.p;
-                sdir = wi;
-                smaxt = norm(dv) - kEps;
-            }
-            if (add) {
-                float4 L = rec[work];
-                rec[work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, 0.0f);
-            }
-            // Russian roulette on the red channel (path_mis.cpp:64-69)
-            float qrr = smin(beta.x, 0.99f);
-            if (!(next1D(rng) > qrr)) {
-                beta = beta / qrr;
-                BRec br;
-                br.wi = to_local(hs.sh, -d);
-                br.wo = V3{0, 0, 1};
-                br.measure = kMeasureUnknown;
-                V3 w = bsdf_sample(B, br, next2D(rng));
-                if (!is_zero(w)) {  // deviation D1: zero-weight samples end the path
-                    beta = beta * w;
-                    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
-                        float pm = bsdf_pdf(B, br);
-                        prev = br.measure == kMeasureDiscrete ? -1.0f : pm;
-                    }
-                    no = hs.p;
-                    nd = to_world(hs.sh, br.wo);
-                    alive = true;
-                }
-            }
-        }
+                                                       SegState seg, int in_sel, WorkDesc wd, float4 *rec,
+                                                       Counters *C) {
+    __shared__ uint32_t s_need[kShadeBlock / 64], s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, q = b * kSeg + tid;
+    const uint32_t n_in = seg.cnt[in_sel][b];
+    PathState ps;
+    ShadowOut so;
+    so.emit = false;
+    bool alive = false;
+    if (tid < n_in) {
+        load_path(in, q, ps);
+        alive = shade_vertex<INTEG>(S, ps, in.hit[q], rec, so);
     }
-
-    // ---- regenerate finished slots from the work counter (one atomic per wave)
-    bool need = !alive;
-    uint64_t mneed = __ballot(need);
-    unsigned long long base = wave_reserve64(&C->next_work, mneed);
-    float nmint = kEps, nmaxt = INF_F;
+    // ---- regenerate from this segment's work stream
+    const bool need = !alive;
+    const uint64_t mneed = __ballot(need), msh = __ballot(so.emit);
+    if (lane_id() == 0) {
+        s_need[wave] = (uint32_t)__popcll(mneed);
+        s_sh[wave] = (uint32_t)__popcll(msh);
+    }
+    const uint32_t cursor = seg.cursor[b];
+    __syncthreads();
+    uint32_t need_off = rank_in(mneed), sh_off = rank_in(msh), need_tot = 0, sh_tot = 0;
+    for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
+        need_off += w < wave ? s_need[w] : 0u;
+        sh_off += w < wave ? s_sh[w] : 0u;
+        need_tot += s_need[w];
+        sh_tot += s_sh[w];
+    }
+    bool fresh = false;
     if (need) {
-        unsigned long long w = base + rank_in(mneed);
+        uint64_t w = stream_work(wd, b, cursor + need_off);
         if (w < wd.total) {
-            work = (uint32_t)w;
-            uint32_t pass = work / wd.M, e = work - pass * wd.M;
-            uint32_t pix = wd.pixels[e];
-            uint32_t W = (uint32_t)S.W;
-            uint32_t y = pix / W, x = pix - y * W;
-            uint64_t sid = (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix;
-            wave_seed(rng, wd.seed, sid);
-            V2 jit = next2D(rng);
-            (void)next2D(rng);  // apertureSample (render.cpp:99)
-            camera_ray(S, (float)x + jit.x, (float)y + jit.y, no, nd, nmint, nmaxt);
-            beta = V3{1, 1, 1};
-            prev = -1.0f;
-            rec[work] = make_float4(0, 0, 0, 0);
-            alive = true;
+            regen_path(S, wd, (uint32_t)w, ps, rec);
+            alive = fresh = true;
         }
     }
-
-    // ---- compact shadow rays and surviving paths
-    uint64_t msh = __ballot(shadow);
-    uint32_t sbase = wave_reserve(&C->shadow_count[sh_sel], msh);
-    if (shadow) {
-        uint32_t i = sbase + rank_in(msh);
-        sq.ray_o[i] = make_float4(so.x, so.y, so.z, kEps);
-        sq.ray_d[i] = make_float4(sdir.x, sdir.y, sdir.z, smaxt);
-        sq.payload[i] = make_float4(contrib.x, contrib.y, contrib.z, __uint_as_float(swork));
+    if (so.emit) {
+        uint32_t i = b * kSeg + sh_off;
+        sq.ray_o[i] = make_float4(so.o.x, so.o.y, so.o.z, kEps);
+        sq.ray_d[i] = make_float4(so.d.x, so.d.y, so.d.z, so.maxt);
+        sq.payload[i] = make_float4(so.contrib.x, so.contrib.y, so.contrib.z, __uint_as_float(so.work));
     }
-    uint64_t mal = __ballot(alive);
-    uint32_t obase = wave_reserve(&C->qcount[in_sel ^ 1], mal);
-    if (lane_id() == 0 && (mal | msh)) {
-        if (mal) atomicAdd(&C->rays_closest, (unsigned long long)__popcll(mal));
-        if (msh) atomicAdd(&C->rays_shadow, (unsigned long long)__popcll(msh));
+    const uint64_t mal = __ballot(alive), mfresh = __ballot(fresh);
+    if (lane_id() == 0) s_al[wave] = (uint32_t)__popcll(mal) | ((uint32_t)__popcll(mfresh) << 16);
+    __syncthreads();
+    uint32_t al_off = rank_in(mal), al_tot = 0, fresh_tot = 0;
+    for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
+        al_off += w < wave ? (s_al[w] & 0xFFFFu) : 0u;
+        al_tot += s_al[w] & 0xFFFFu;
+        fresh_tot += s_al[w] >> 16;
     }
-    if (alive) {
-        uint32_t i = obase + rank_in(mal);
-        out.ray_o[i] = make_float4(no.x, no.y, no.z, nmint);
-        out.ray_d[i] = make_float4(nd.x, nd.y, nd.z, nmaxt);
-        out.thr[i] = make_float4(beta.x, beta.y, beta.z, prev);
-        out.rng[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), (uint32_t)rng.inc, (uint32_t)(rng.inc >> 32));
-        out.work[i] = work;
+    if (alive) store_path(out, b * kSeg + al_off, ps);
+    if (tid == 0) {
+        seg.cnt[in_sel ^ 1][b] = al_tot;
+        seg.shcnt[b] = sh_tot;
+        seg.cursor[b] = cursor + need_tot;
+        uint4 st = seg.stats[b];
+        seg.stats[b] = make_uint4(st.x + al_tot, st.y + sh_tot, st.z + fresh_tot, st.w);
+        if (stream_work(wd, b, cursor) < wd.total && stream_work(wd, b, cursor + need_tot) >= wd.total) {
+            // the last segment to run dry tells the host (system-scope store to
+            // host-mapped memory) -- no per-iteration readback is needed
+            uint32_t n = atomicAdd(&C->exhausted, 1u) + 1u;
+            // progress hint: plain system-scope store (no PCIe atomics needed)
+            __hip_atomic_store(wd.done_flag + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (n == wd.G) __hip_atomic_store(wd.done_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
+// Runs every path still queued to completion, one thread per path: the
+// Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
+// bounce) would otherwise cost three launches per bounce.
+template <int STACK, int INTEG>
+__global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene S, PathQueue Q, SegState seg, int sel,
+                                                        float4 *rec) {
+    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
+    if (idx >= seg.cnt[sel][sg]) return;
+    const uint32_t q = sg * kSeg + idx;
+    PathState ps;
+    load_path(Q, q, ps);
+    float4 h = Q.hit[q];
+    uint32_t rays = 0;
+    for (;;) {
+        ShadowOut so;
+        bool alive = shade_vertex<INTEG>(S, ps, h, rec, so);
+        if (so.emit) {
+            TRay r{so.o, so.d, V3{0, 0, 0}, kEps, so.maxt};
+            float t, u, v;
+            uint32_t p;
+            ++rays;
+            if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) {
+                float4 L = rec[so.work];
+                rec[so.work] = make_float4(L.x + so.contrib.x, L.y + so.contrib.y, L.z + so.contrib.z, 0.0f);
+            }
+        }
+        if (!alive) break;
+        TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
+        float t, u, v;
+        uint32_t p;
+        ++rays;
+        traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
+        h = make_float4(t, __uint_as_float(p), u, v);
+    }
+    atomicAdd(&seg.stats[sg].w, rays);
+}
+
 // ------------------------------------------------------------------ film splat
-// ImageBlock::put(pos, val) (block.cpp:93-122) into an LDS tile per 32x32
-// block, then ImageBlock::put(block) (block.cpp:124-133) into the film.
+// ImageBlock::put(pos, val) (block.cpp:93-122) for every sample of one 32x32
+// block and a range of passes, then ImageBlock::put(block) (block.cpp:124-133)
+// into the film.  A thread owns one pixel: all samples of that pixel fall in
+// the same (2B+1)^2 window around it, so the thread sums the filtered samples
+// of all its passes in registers and touches the LDS tile once per window
+// cell instead of once per sample and cell.
+template <int B>
 __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 *rec, SplatDesc sd, float *film,
                                                       Counters *C) {
-    extern __shared__ float tile[];
+    constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1;
+    __shared__ float tile[TS * TS * 4];
     __shared__ float ftab[NORI_FILTER_RESOLUTION + 1];
-    const int B = S.border, TS = NORI_BLOCK_SIZE + 2 * B;
     int4 bi = sd.blocks[blockIdx.x];
-    int ox = bi.x, oy = bi.y, bw = bi.z & 0xFFFF, bh = bi.z >> 16;
-    uint32_t off = (uint32_t)bi.w;
-    uint32_t p0 = blockIdx.y * sd.passes_per_wg, p1 = min(sd.passes, p0 + sd.passes_per_wg);
+    const int ox = bi.x, oy = bi.y, bw = bi.z & 0xFFFF, bh = bi.z >> 16;
+    const uint32_t off = (uint32_t)bi.w;
+    const uint32_t p0 = blockIdx.y * sd.passes_per_wg, p1 = min(sd.passes, p0 + sd.passes_per_wg);
     for (int i = threadIdx.x; i < TS * TS * 4; i += kSplatBlock) tile[i] = 0.0f;
     if (threadIdx.x <= NORI_FILTER_RESOLUTION) ftab[threadIdx.x] = S.filter[threadIdx.x];
     __syncthreads();
-    const uint32_t npix = (uint32_t)(bw * bh);
-    const uint32_t n = (p1 - p0) * npix;
+    const int npix = bw * bh;
     const float rad = S.filter_radius, lk = S.lookup;
     const uint64_t WH = (uint64_t)S.W * (uint64_t)S.H;
     uint32_t inval = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += kSplatBlock) {
-        uint32_t pl = i / npix, j = i - pl * npix;
-        uint32_t p = p0 + pl;
-        int ly = (int)(j / (uint32_t)bw), lx = (int)(j - (uint32_t)ly * (uint32_t)bw);
-        float4 L = rec[(size_t)p * sd.M + off + j];
-        int x = ox + lx, y = oy + ly;
-        uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
-        Pcg r;
-        wave_seed(r, sd.seed, sid);
-        V2 jit = next2D(r);
-        float psx = (float)x + jit.x, psy = (float)y + jit.y;
-        // Color3f::isValid (common.cpp:224-231)
-        bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
-        if (!valid) {
-            ++inval;
-            continue;
-        }
-        float px = psx - 0.5f - (float)(ox - B), py = psy - 0.5f - (float)(oy - B);
-        int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
-        int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
-        for (int yy = y0; yy <= y1; ++yy) {
-            float wy = ftab[(int)(fabsf((float)yy - py) * lk)];
-            for (int xx = x0; xx <= x1; ++xx) {
-                float wx = ftab[(int)(fabsf((float)xx - px) * lk)];
-                float *c = tile + 4 * (yy * TS + xx);
-                atomicAdd(c + 0, (L.x * wx) * wy);
-                atomicAdd(c + 1, (L.y * wx) * wy);
-                atomicAdd(c + 2, (L.z * wx) * wy);
-                atomicAdd(c + 3, (1.0f * wx) * wy);
+    for (int j = threadIdx.x; j < npix; j += kSplatBlock) {
+        const int ly = j / bw, lx = j - ly * bw, x = ox + lx, y = oy + ly;
+        float acc[K][K][4];
+#pragma unroll
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = acc[a][c][2] = acc[a][c][3] = 0.0f;
+        bool any = false;
+        for (uint32_t p = p0; p < p1; ++p) {
+            float4 L = rec[(size_t)p * sd.M + off + j];
+            uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
+            Pcg r;
+            wave_seed(r, sd.seed, sid);
+            V2 jit = next2D(r);
+            // Color3f::isValid (common.cpp:224-231): invalid samples are dropped
+            bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
+            if (!valid) {
+                ++inval;
+                continue;
             }
+            any = true;
+            float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
+            int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
+            int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
+            float wx[K], wy[K];
+#pragma unroll
+            for (int d = 0; d < K; ++d) {
+                int cx = lx + d, cy = ly + d;  // tile column / row of window cell d
+                int kx = min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION);
+                int ky = min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION);
+                wx[d] = (cx >= x0 && cx <= x1) ? ftab[kx] : 0.0f;
+                wy[d] = (cy >= y0 && cy <= y1) ? ftab[ky] : 0.0f;
+            }
+#pragma unroll
+            for (int a = 0; a < K; ++a)
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    acc[a][c][0] += (L.x * wx[c]) * wy[a];
+                    acc[a][c][1] += (L.y * wx[c]) * wy[a];
+                    acc[a][c][2] += (L.z * wx[c]) * wy[a];
+                    acc[a][c][3] += (1.0f * wx[c]) * wy[a];
+                }
+        }
+        if (any) {
+#pragma unroll
+            for (int a = 0; a < K; ++a)
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    float *t = tile + 4 * ((ly + a) * TS + (lx + c));
+                    if (acc[a][c][3] != 0.0f || acc[a][c][0] != 0.0f || acc[a][c][1] != 0.0f || acc[a][c][2] != 0.0f) {
+                        atomicAdd(t + 0, acc[a][c][0]);
+                        atomicAdd(t + 1, acc[a][c][1]);
+                        atomicAdd(t + 2, acc[a][c][2]);
+                        atomicAdd(t + 3, acc[a][c][3]);
+                    }
+                }
         }
     }
     if (inval) atomicAdd(&C->invalid, (unsigned long long)inval);
@@ -554,6 +723,7 @@ static hipError_t trace_dispatch(const DevScene &S, const float4 *rays, uint32_t
                                  hipStream_t st) {
     dim3 g((n + kTraceBlock - 1) / kTraceBlock), b(kTraceBlock);
     switch (stack) {
+    case 0: hipLaunchKernelGGL((k_trace<0, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 8: hipLaunchKernelGGL((k_trace<8, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 16: hipLaunchKernelGGL((k_trace<16, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 32: hipLaunchKernelGGL((k_trace<32, ANY>), g, b, 0, st, S, rays, n, hits); break;
@@ -569,47 +739,75 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 }
 
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                        Counters *C, int in_sel, int sh_sel, const WorkDesc &wd, float4 *rec, uint32_t pool,
+                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                         hipStream_t st) {
-    dim3 g(pool / kShadeBlock), b(kShadeBlock);
+    dim3 g(wd.G), b(kShadeBlock);
     if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS>), g, b, 0, st, S, in, out, sq, C, in_sel, sh_sel, wd, rec);
+        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C);
     else
-        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS>), g, b, 0, st, S, in, out, sq, C, in_sel, sh_sel, wd, rec);
+        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C);
     return hipGetLastError();
 }
 
-hipError_t launch_extend(const DevScene &S, const PathQueue &q, Counters *C, int q_sel, int reset_q, int reset_sh,
-                         uint32_t pool, int stack, hipStream_t st) {
-    dim3 g(pool / kTraceBlock), b(kTraceBlock);
+hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
+                         hipStream_t st) {
+    dim3 g(2 * G), b(kTraceBlock);
     switch (stack) {
-    case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, C, q_sel, reset_q, reset_sh); break;
-    case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, C, q_sel, reset_q, reset_sh); break;
-    case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, C, q_sel, reset_q, reset_sh); break;
-    default: hipLaunchKernelGGL(k_extend<64>, g, b, 0, st, S, q, C, q_sel, reset_q, reset_sh); break;
+    case 0: hipLaunchKernelGGL(k_extend<0>, g, b, 0, st, S, q, cnt); break;
+    case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt); break;
+    case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, cnt); break;
+    case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, cnt); break;
+    default: hipLaunchKernelGGL(k_extend<64>, g, b, 0, st, S, q, cnt); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, Counters *C, int sh_sel, float4 *rec,
-                         uint32_t pool, int stack, hipStream_t st) {
-    dim3 g(pool / kTraceBlock), b(kTraceBlock);
+hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
+                         int stack, hipStream_t st) {
+    dim3 g(2 * G), b(kTraceBlock);
     switch (stack) {
-    case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, C, sh_sel, rec); break;
-    case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, C, sh_sel, rec); break;
-    case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, C, sh_sel, rec); break;
-    default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, C, sh_sel, rec); break;
+    case 0: hipLaunchKernelGGL(k_shadow<0>, g, b, 0, st, S, sq, shcnt, rec); break;
+    case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec); break;
+    case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec); break;
+    case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec); break;
+    default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec); break;
     }
+    return hipGetLastError();
+}
+
+template <int INTEG>
+static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
+                            uint32_t G, int stack, hipStream_t st) {
+    dim3 g(2 * G), b(kTraceBlock);
+    switch (stack) {
+    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
+    }
+}
+hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
+                         uint32_t G, int stack, hipStream_t st) {
+    if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
+        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, G, stack, st);
+    else
+        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, G, stack, st);
     return hipGetLastError();
 }
 
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st) {
     if (nblocks == 0 || sd.passes == 0) return hipSuccess;
-    int TS = NORI_BLOCK_SIZE + 2 * S.border;
-    size_t lds = sizeof(float) * 4 * (size_t)TS * TS;
     dim3 g(nblocks, (sd.passes + sd.passes_per_wg - 1) / sd.passes_per_wg), b(kSplatBlock);
-    hipLaunchKernelGGL(k_splat, g, b, lds, st, S, rec, sd, film, C);
+    switch (S.border) {
+    case 0: hipLaunchKernelGGL(k_splat<0>, g, b, 0, st, S, rec, sd, film, C); break;
+    case 1: hipLaunchKernelGGL(k_splat<1>, g, b, 0, st, S, rec, sd, film, C); break;
+    case 2: hipLaunchKernelGGL(k_splat<2>, g, b, 0, st, S, rec, sd, film, C); break;
+    case 3: hipLaunchKernelGGL(k_splat<3>, g, b, 0, st, S, rec, sd, film, C); break;
+    case 4: hipLaunchKernelGGL(k_splat<4>, g, b, 0, st, S, rec, sd, film, C); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

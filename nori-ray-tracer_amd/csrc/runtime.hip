@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -23,6 +24,7 @@
 namespace nori {
 
 static thread_local std::string g_last_error;
+constexpr uint32_t kScanMaxPrims = 64;  // wave-uniform scan instead of BVH at or below this
 
 #define HIP_TRY(x)                                                                                       \
     do {                                                                                                 \
@@ -139,9 +141,10 @@ struct nori_gpu_ctx {
     std::atomic<int> cancel{0};
     std::atomic<float> progress{1.0f};
     // render state
-    DevBuf q[2][6], sq[3], rec, counters, pixels, blocks, film;
+    DevBuf q[2][6], sq[3], seg[4], segstats, rec, counters, pixels, blocks, film;
     uint32_t pool_cap = 0;
-    uint32_t *pinned = nullptr;  // readback ring
+    uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
+    uint32_t *pinned_dev = nullptr;  // device view of `pinned`
     std::vector<hipEvent_t> ring;
     ~nori_gpu_ctx() {
         for (auto e : ring) (void)hipEventDestroy(e);
@@ -290,6 +293,14 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     else if (bvh.depth <= 32) c.stack = 32;
     else if (bvh.depth <= 64) c.stack = 64;
     else throw NoriException(NORI_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+    // Traversal strategy: scenes of at most kScanMaxPrims primitives are
+    // intersected by a wave-uniform scan (scalar loads, no divergence), larger
+    // ones by per-lane BVH traversal.  NORI_TRAVERSAL=bvh|scan overrides.
+    const char *mode = std::getenv("NORI_TRAVERSAL");
+    bool scan = off <= kScanMaxPrims;
+    if (mode && std::string(mode) == "bvh") scan = false;
+    if (mode && std::string(mode) == "scan") scan = true;
+    if (scan) c.stack = 0;
 
     std::vector<float> pos(4 * (size_t)d.num_vertices), nrm(4 * (size_t)d.num_vertices);
     for (uint32_t v = 0; v < d.num_vertices; ++v)
@@ -324,6 +335,8 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.cdf = c.cdf.as<float>();
     S.num_emitters = d.num_emitters;
     S.num_nodes = bvh.num_nodes;
+    S.num_prims = off;
+    for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     const nori_camera_desc &cam = d.camera;
     c.cam = cam;
     if (cam.width <= 0 || cam.height <= 0) throw NoriException(NORI_ERR_INVALID, "bad output size");
@@ -339,7 +352,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.filter_radius = cam.filter_radius;
     S.lookup = NORI_FILTER_RESOLUTION / cam.filter_radius;
     S.border = film_border(cam);
-    if (S.border > 8) throw NoriException(NORI_ERR_UNSUPPORTED, "filter radius above 8.5 pixels");
+    if (S.border > 4) throw NoriException(NORI_ERR_UNSUPPORTED, "filter radius above 4.5 pixels");
     S.integrator = d.integrator;
     S.has_medium = d.medium.present;
 }
@@ -355,6 +368,8 @@ void ensure_pool(nori_gpu_ctx &c, uint32_t pool) {
         c.q[b][5].ensure(4 * (size_t)pool);
     }
     for (int k = 0; k < 3; ++k) c.sq[k].ensure(16 * (size_t)pool);
+    for (int k = 0; k < 4; ++k) c.seg[k].ensure(4 * (size_t)(pool / kSeg));
+    c.segstats.ensure(16 * (size_t)(pool / kSeg));
     c.pool_cap = pool;
 }
 
@@ -421,7 +436,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     const uint32_t passes = rd.pass_count ? rd.pass_count : 0;
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
     uint32_t pool = rd.path_pool ? rd.path_pool : (1u << 21);
-    pool = (pool + 255) / 256 * 256;
+    pool = std::max<uint32_t>(kSeg, (pool + kSeg - 1) / kSeg * kSeg);
     ensure_pool(c, pool);
     // sample-record budget: chunks of passes, each < 2^31 records
     const size_t rec_budget = (size_t)6 << 30;
@@ -441,7 +456,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipMemsetAsync(film, 0, film_elems * sizeof(float), c.stream));
     }
     if (!c.pinned) {
-        HIP_TRY(hipHostMalloc((void **)&c.pinned, kRing * 32, hipHostMallocDefault));
+        // host-mapped, coherent: the shade kernel stores the completion flag here
+        HIP_TRY(hipHostMalloc((void **)&c.pinned, 256, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer((void **)&c.pinned_dev, c.pinned, 0));
         c.ring.resize(kRing);
         for (auto &e : c.ring) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
@@ -471,30 +488,41 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         spans.push_back(s);
     };
     bool cancelled = false;
+    const uint32_t G = pool / kSeg;
+    SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
+                 c.segstats.as<uint4>()};
+    std::vector<uint4> hstats(G);
+    uint64_t finish_rays = 0, samples_started = 0;
     for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
         uint32_t np = std::min(chunk, passes - p0);
-        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed};
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev};
+        __atomic_store_n(&c.pinned[0], 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(&c.pinned[1], 0u, __ATOMIC_RELEASE);
+        // segments whose stream is empty from the start count as exhausted
+        uint32_t empty = 0;
+        for (uint32_t b = 0; b < G; ++b) empty += stream_work(wd, b, 0) >= wd.total;
         HIP_TRY(hipMemsetAsync(C, 0, sizeof(Counters), c.stream));
+        HIP_TRY(hipMemcpyAsync(&C->exhausted, &empty, 4, hipMemcpyHostToDevice, c.stream));
+        HIP_TRY(hipMemsetAsync(seg.cnt[0], 0, 4 * (size_t)G, c.stream));
+        HIP_TRY(hipMemsetAsync(seg.cursor, 0, 4 * (size_t)G, c.stream));
+        HIP_TRY(hipMemsetAsync(seg.stats, 0, 16 * (size_t)G, c.stream));
+        int last_out = 0;
         for (uint64_t it = 0;; ++it) {
-            int in = (int)(it & 1), out = in ^ 1, sh = (int)(it & 1);
-            timed(2, [&] { return launch_shade(S, Q[in], Q[out], sq, C, in, sh, wd, c.rec.as<float4>(), pool, c.stream); });
-            timed(0, [&] { return launch_extend(S, Q[out], C, out, in, sh ^ 1, pool, c.stack, c.stream); });
-            timed(1, [&] { return launch_shadow(S, sq, C, sh, c.rec.as<float4>(), pool, c.stack, c.stream); });
-            int slot = (int)(it % kRing);
-            // snapshot {qcount[0..1], shadow_count[0..1], next_work}
-            HIP_TRY(hipMemcpyAsync(c.pinned + 8 * slot, C, 32, hipMemcpyDeviceToHost, c.stream));
-            HIP_TRY(hipEventRecord(c.ring[slot], c.stream));
+            int in = (int)(it & 1), out = in ^ 1;
+            last_out = out;
+            timed(2, [&] { return launch_shade(S, Q[in], Q[out], sq, seg, in, wd, c.rec.as<float4>(), C, c.stream); });
+            timed(0, [&] { return launch_extend(S, Q[out], seg.cnt[out], G, c.stack, c.stream); });
+            timed(1, [&] { return launch_shadow(S, sq, seg.shcnt, c.rec.as<float4>(), G, c.stack, c.stream); });
+            HIP_TRY(hipEventRecord(c.ring[it % kRing], c.stream));
             ++iters;
             if (it >= (uint64_t)kLookahead) {
-                uint64_t chk = it - kLookahead;
-                int cs = (int)(chk % kRing);
-                HIP_TRY(hipEventSynchronize(c.ring[cs]));
-                const uint32_t *snap = c.pinned + 8 * cs;
-                int chk_out = (int)((chk & 1) ^ 1);
-                uint64_t nw;
-                std::memcpy(&nw, snap + 4, 8);
-                c.progress = (float)std::min(1.0, (double)(done_before + std::min<uint64_t>(nw, wd.total)) / (double)total_all);
-                if (snap[chk_out] == 0 && nw >= wd.total) break;
+                // bound the run-ahead of the host to kLookahead iterations
+                HIP_TRY(hipEventSynchronize(c.ring[(it - kLookahead) % kRing]));
+                uint32_t exhausted = __atomic_load_n(&c.pinned[1], __ATOMIC_ACQUIRE);
+                c.progress = (float)std::min(1.0, (double)done_before / (double)total_all +
+                                                      (double)np / passes * exhausted / G);
+                // every work id has been handed out: finish the remaining paths in one launch
+                if (__atomic_load_n(&c.pinned[0], __ATOMIC_ACQUIRE)) break;
                 if (c.cancel.load()) {
                     cancelled = true;
                     break;
@@ -502,18 +530,27 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             }
         }
         if (cancelled) break;
-        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 16)),
+        timed(4, [&] { return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stack, c.stream); });
+        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)),
                      c.blocks.as<int4>(), rd.seed};
         timed(3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream); });
         Counters hc;
         HIP_TRY(hipMemcpyAsync(&hc, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
+        HIP_TRY(hipMemcpyAsync(hstats.data(), seg.stats, 16 * (size_t)G, hipMemcpyDeviceToHost, c.stream));
         HIP_TRY(hipStreamSynchronize(c.stream));
-        rays_c += hc.rays_closest;
-        rays_s += hc.rays_shadow;
+        for (const uint4 &st : hstats) {
+            rays_c += st.x;
+            rays_s += st.y;
+            samples_started += st.z;
+            finish_rays += st.w;
+        }
         invalid += hc.invalid;
         done_before += wd.total;
     }
-    double kms[4] = {0, 0, 0, 0};
+    if (samples_started != done_before && !cancelled)
+        throw NoriException(NORI_ERR_INVALID, "internal: started " + std::to_string(samples_started) + " of " +
+                                                  std::to_string(done_before) + " samples");
+    double kms[5] = {0, 0, 0, 0, 0};
     if (timing) {
         HIP_TRY(hipStreamSynchronize(c.stream));
         for (const Span &s : spans) {
@@ -544,6 +581,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         stats->ms_shadow = kms[1];
         stats->ms_shade = kms[2];
         stats->ms_splat = kms[3];
+        stats->ms_finish = kms[4];
+        stats->rays_finish = finish_rays;
     }
     if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
     return NORI_OK;

@@ -9,8 +9,12 @@ Tolerances:
   few ulp (ROCm device library vs glibc), which flips rare branches, so the
   bar is per-pixel L2 < 1e-3 on linear RGB (BASELINE.json north_star).
 """
+import os
+
 import numpy as np
 import pytest
+
+import synth
 
 import nori_amd
 import pyoracle
@@ -43,10 +47,33 @@ def _compare_hits(g, c):
     assert same.mean() > 0.999, same.mean()
 
 
-@pytest.fixture(scope="module")
-def cbox(built):
+def _renderer(scene, mode=None):
+    """GpuRenderer with a forced traversal mode ('scan' or 'bvh'; None = automatic)."""
+    old = os.environ.get("NORI_TRAVERSAL")
+    if mode:
+        os.environ["NORI_TRAVERSAL"] = mode
+    try:
+        return nori_amd.GpuRenderer(scene, 0)
+    finally:
+        if old is None:
+            os.environ.pop("NORI_TRAVERSAL", None)
+        else:
+            os.environ["NORI_TRAVERSAL"] = old
+
+
+@pytest.fixture(scope="module", params=["scan", "bvh"])
+def cbox(built, request):
     s = nori_amd.load_scene(scene_path("pa4", "cbox", "cbox_path_mis.xml"), 64, 64, 16)
-    r = nori_amd.GpuRenderer(s, 0)
+    r = _renderer(s, request.param)
+    yield s, r, pyoracle.OracleScene(s)
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def hfield(built, tmp_path_factory):
+    xml = synth.heightfield_scene(str(tmp_path_factory.mktemp("hf")), n=48, width=96, height=72, spp=8)
+    s = nori_amd.load_scene(xml)
+    r = _renderer(s)
     yield s, r, pyoracle.OracleScene(s)
     r.close()
 
@@ -109,3 +136,33 @@ def test_furnace_gpu(built, tmp_path):
         val = float((img[0, 0] * [0.212671, 0.715160, 0.072169]).sum())
         ok, p = students_t_test(val, var_o, ref, 40000, 0.01, len(meta["references"]))
         assert ok, (integ, ref, val, p)
+
+
+def test_trace_large_mesh_bvh(hfield):
+    s, r, o = hfield
+    rays = np.concatenate([_rays(30000, 5, [-0.9, 0.05, -0.9], [0.9, 1.5, 0.9]),
+                           _rays(5000, 6, [-3, -1, -3], [3, 3, 6], mint=0.01)])
+    _compare_hits(r.trace(rays), o.trace(rays))
+    sh = rays.copy()
+    sh[:, 7] = np.random.default_rng(7).uniform(0.01, 2.0, size=sh.shape[0])
+    assert ((r.trace(sh, any_hit=True)["prim"] >= 0) == (o.trace(sh, any_hit=True)["prim"] >= 0)).all()
+
+
+def test_render_large_mesh_matches_oracle(hfield):
+    s, r, o = hfield
+    gpu = nori_amd.develop(s, r.render())
+    cpu = nori_amd.develop(s, o.render(rng="wave"))
+    l2 = float(np.mean((gpu - cpu) ** 2))
+    print(f"heightfield microfacet path_mis: L2 {l2:.3e}")
+    assert np.isfinite(gpu).all()
+    assert l2 < L2_TOL
+
+
+@pytest.mark.parametrize("mode", ["scan", "bvh"])
+def test_render_modes_agree(built, mode):
+    s = nori_amd.load_scene(scene_path("pa4", "cbox", "cbox_path_mis.xml"), 64, 48, 8)
+    r = _renderer(s, mode)
+    gpu = nori_amd.develop(s, r.render())
+    r.close()
+    cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
+    assert float(np.mean((gpu - cpu) ** 2)) < L2_TOL
