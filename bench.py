@@ -128,11 +128,13 @@ def main():
 
     def step(timing=False):
         if world > 1:
+            from nori_amd import distributed as nd
+
             film_t.zero_()
             torch.cuda.synchronize()
-            r.render(passes=args.spp, pass_begin=rank * args.spp, device_ptr=film_t.data_ptr(),
-                     path_pool=args.pool, timing=timing)
-            dist.all_reduce(film_t)
+            pb, pc = nd.pass_range(rank, args.spp)
+            r.render(passes=pc, pass_begin=pb, device_ptr=film_t.data_ptr(), path_pool=args.pool, timing=timing)
+            nd.reduce_film(film_t, dist)
         else:
             r.render(passes=args.spp, path_pool=args.pool, timing=timing)
         return r.last_stats
@@ -182,7 +184,7 @@ def main():
             "config": {"workload": f"cbox_path_mis {args.width}x{args.height}@{args.spp}spp",
                        "scene": "scenes/pa4/cbox/cbox_path_mis.xml", "integrator": "path_mis",
                        "parallelism": f"pass-range sharding x{world}, RCCL film all_reduce" if world > 1
-                       else "single GPU", "path_pool": args.pool or 2097152},
+                       else "single GPU", "path_pool": args.pool or 4194304},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_extend (closest-hit traversal)",

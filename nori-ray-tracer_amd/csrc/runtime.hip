@@ -435,7 +435,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     const uint32_t M = (uint32_t)pixels.size();
     const uint32_t passes = rd.pass_count ? rd.pass_count : 0;
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
-    uint32_t pool = rd.path_pool ? rd.path_pool : (1u << 21);
+    // default pool: 4M paths in flight (~0.9 GB of queues); measured best among
+    // 256K..4M on cbox (larger pools hide the shade kernel's memory latency)
+    uint32_t pool = rd.path_pool ? rd.path_pool : (1u << 22);
     pool = std::max<uint32_t>(kSeg, (pool + kSeg - 1) / kSeg * kSeg);
     ensure_pool(c, pool);
     // sample-record budget: chunks of passes, each < 2^31 records
