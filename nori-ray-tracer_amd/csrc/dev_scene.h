@@ -64,7 +64,29 @@ struct DevScene {
     int32_t has_medium;
     float mbox_min[3], mbox_max[3];
     float sigma_t[3], albedo[3];
+    // Small scenes: every table above packed into one blob (byte offsets),
+    // which latency-bound kernels stage into LDS (blob_bytes == 0: none).
+    const float4 *blob;
+    uint32_t blob_bytes;
+    uint32_t off_prims, off_vidx, off_pos, off_nrm, off_pshape, off_shapes, off_bsdfs, off_emitters, off_cdf,
+        off_nodes;
 };
+
+// A copy of S whose small-scene tables point into `lds` (the staged blob).
+ND DevScene scene_in_lds(const DevScene &S, const char *lds) {
+    DevScene L = S;
+    L.prims = reinterpret_cast<const float4 *>(lds + S.off_prims);
+    L.tri_vidx = reinterpret_cast<const uint32_t *>(lds + S.off_vidx);
+    L.pos = reinterpret_cast<const float4 *>(lds + S.off_pos);
+    L.nrm = reinterpret_cast<const float4 *>(lds + S.off_nrm);
+    L.prim_shape = reinterpret_cast<const uint32_t *>(lds + S.off_pshape);
+    L.shapes = reinterpret_cast<const DevShape *>(lds + S.off_shapes);
+    L.bsdfs = reinterpret_cast<const DevBsdf *>(lds + S.off_bsdfs);
+    L.emitters = reinterpret_cast<const DevEmitter *>(lds + S.off_emitters);
+    L.cdf = reinterpret_cast<const float *>(lds + S.off_cdf);
+    L.nodes = reinterpret_cast<const float4 *>(lds + S.off_nodes);
+    return L;
+}
 
 struct PathQueue {
     float4 *ray_o;

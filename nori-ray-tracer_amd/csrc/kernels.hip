@@ -585,11 +585,23 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathQueue in,
 // Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
 // bounce) would otherwise cost three launches per bounce.
 template <int STACK, int INTEG>
-__global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene S, PathQueue Q, SegState seg, int sel,
+__global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec) {
     __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
-    if (idx >= seg.cnt[sel][sg]) return;
+    const uint32_t n = seg.cnt[sel][sg];
+    if ((blockIdx.x & 1) * kTraceBlock >= n) return;  // whole block idle
+    // Each bounce of a tail path is a chain of dependent reads of small
+    // tables; for small scenes they are staged into LDS first so the chain
+    // runs at LDS latency instead of L2 latency.
+    DevScene S = Sg;
+    if (Sg.blob_bytes) {
+        for (uint32_t i = threadIdx.x; i < Sg.blob_bytes / 16; i += kTraceBlock) blob_lds[i] = Sg.blob[i];
+        __syncthreads();
+        S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
+    }
+    if (idx >= n) return;
     const uint32_t q = sg * kSeg + idx;
     PathState ps;
     load_path(Q, q, ps);
@@ -780,11 +792,11 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
                             uint32_t G, int stack, hipStream_t st) {
     dim3 g(2 * G), b(kTraceBlock);
     switch (stack) {
-    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, 0, st, S, Q, seg, sel, rec); break;
+    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
     }
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,

@@ -25,6 +25,7 @@ namespace nori {
 
 static thread_local std::string g_last_error;
 constexpr uint32_t kScanMaxPrims = 64;  // wave-uniform scan instead of BVH at or below this
+constexpr size_t kBlobMaxBytes = 48 << 10;  // small-scene blob staged into LDS
 
 #define HIP_TRY(x)                                                                                       \
     do {                                                                                                 \
@@ -134,8 +135,9 @@ struct nori_gpu_ctx {
     hipStream_t stream = nullptr;
     DevScene S{};
     nori_camera_desc cam{};
-    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf;
-    int stack = 8;
+    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, blob;
+    int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
+    int bvh_stack = 8;   // LDS stack depth of the BVH (tail finisher)
     uint32_t bvh_depth = 0, bvh_nodes = 0, num_prims = 0;
     size_t scene_bytes = 0;
     std::atomic<int> cancel{0};
@@ -300,6 +302,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     bool scan = off <= kScanMaxPrims;
     if (mode && std::string(mode) == "bvh") scan = false;
     if (mode && std::string(mode) == "scan") scan = true;
+    c.bvh_stack = c.stack;  // the tail finisher always walks the BVH: shorter critical path per lone lane
     if (scan) c.stack = 0;
 
     std::vector<float> pos(4 * (size_t)d.num_vertices), nrm(4 * (size_t)d.num_vertices);
@@ -321,6 +324,28 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     c.emitters.upload(emitters);
     c.cdf.upload(cdf);
     c.scene_bytes = c.nodes.bytes + c.prims.bytes;
+    // small-scene blob (staged into LDS by the tail finisher)
+    std::vector<char> blob;
+    uint32_t offs[10] = {0};
+    auto put = [&](int k, const void *p, size_t n) {
+        while (blob.size() % 16) blob.push_back(0);
+        offs[k] = (uint32_t)blob.size();
+        const char *b = static_cast<const char *>(p);
+        blob.insert(blob.end(), b, b + n);
+    };
+    put(0, bvh.prims.data(), bvh.prims.size() * 4);
+    put(1, tri_vidx.data(), tri_vidx.size() * 4);
+    put(2, pos.data(), pos.size() * 4);
+    put(3, nrm.data(), nrm.size() * 4);
+    put(4, prim_shape.data(), prim_shape.size() * 4);
+    put(5, shapes.data(), shapes.size() * sizeof(DevShape));
+    put(6, bsdfs.data(), bsdfs.size() * sizeof(DevBsdf));
+    put(7, emitters.data(), emitters.size() * sizeof(DevEmitter));
+    put(8, cdf.data(), cdf.size() * 4);
+    put(9, bvh.nodes.data(), bvh.nodes.size() * 4);
+    while (blob.size() % 16) blob.push_back(0);
+    const bool use_blob = c.stack == 0 && blob.size() <= kBlobMaxBytes;
+    if (use_blob) c.blob.upload(blob);
 
     DevScene &S = c.S;
     S.nodes = c.nodes.as<float4>();
@@ -337,6 +362,18 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.num_nodes = bvh.num_nodes;
     S.num_prims = off;
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
+    S.blob = use_blob ? c.blob.as<float4>() : nullptr;
+    S.blob_bytes = use_blob ? (uint32_t)blob.size() : 0u;
+    S.off_prims = offs[0];
+    S.off_vidx = offs[1];
+    S.off_pos = offs[2];
+    S.off_nrm = offs[3];
+    S.off_pshape = offs[4];
+    S.off_shapes = offs[5];
+    S.off_bsdfs = offs[6];
+    S.off_emitters = offs[7];
+    S.off_cdf = offs[8];
+    S.off_nodes = offs[9];
     const nori_camera_desc &cam = d.camera;
     c.cam = cam;
     if (cam.width <= 0 || cam.height <= 0) throw NoriException(NORI_ERR_INVALID, "bad output size");
@@ -532,7 +569,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             }
         }
         if (cancelled) break;
-        timed(4, [&] { return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stack, c.stream); });
+        timed(4, [&] { return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.bvh_stack, c.stream); });
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)),
                      c.blocks.as<int4>(), rd.seed};
         timed(3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream); });
