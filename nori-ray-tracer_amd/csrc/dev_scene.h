@@ -117,15 +117,23 @@ struct WorkDesc {
     uint64_t seed;
     uint32_t G;              // segments
     uint32_t *done_flag;     // host-mapped: set when the last segment exhausts its stream
+    uint32_t rot;            // stream rotation (stream_rotation)
 };
-// Round j hands segment b the chunk (b + j*kRotate) mod G of that round, so a
-// segment sees a different part of the image every round (path lengths vary
-// strongly across the image; a fixed pixel set per segment drains unevenly).
-constexpr uint32_t kRotate = 1031;  // odd: coprime with the power-of-two G
+// Round j hands segment b the chunk (b + j*rot) mod G of that round.  Path
+// lengths vary strongly across the image, so every segment's stream must
+// sample the whole image evenly or the segments run dry at very different
+// times: rot = chunks per pass / rounds spreads a segment's rounds over the
+// pass at equal strides (each round is a shift, so any rot is a bijection).
 NHD uint64_t stream_work(const WorkDesc &wd, uint32_t b, uint32_t p) {
     uint64_t j = p / kSeg;
-    uint64_t col = (b + j * kRotate) % wd.G;
+    uint64_t col = (b + j * wd.rot) % wd.G;
     return (j * wd.G + col) * kSeg + (p % kSeg);
+}
+inline uint32_t stream_rotation(uint64_t total, uint32_t M, uint32_t G) {
+    uint64_t chunks_per_pass = (M + kSeg - 1) / kSeg;
+    uint64_t rounds = (total + (uint64_t)G * kSeg - 1) / ((uint64_t)G * kSeg);
+    uint64_t r = rounds ? chunks_per_pass / rounds : 1;
+    return (uint32_t)(r ? r : 1);
 }
 
 struct SegState {

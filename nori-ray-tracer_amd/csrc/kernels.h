@@ -8,7 +8,15 @@ namespace nori {
 
 constexpr int kShadeBlock = 256;   // shade / regen work-group size
 constexpr int kTraceBlock = 128;   // traversal work-group size (LDS stack columns)
+#ifndef NORI_TRACE_GROUP
+#define NORI_TRACE_GROUP 4
+#endif
+constexpr int kTraceGroup = NORI_TRACE_GROUP;  // segments per extend/shadow work-group
 constexpr int kSplatBlock = 256;
+#ifndef NORI_SHADE_LDS_MAX
+#define NORI_SHADE_LDS_MAX 16384
+#endif
+constexpr uint32_t kShadeLdsMax = NORI_SHADE_LDS_MAX;  // largest scene blob the shade kernel stages in LDS
 
 struct SplatDesc {
     uint32_t M;               // pixels per pass in the work list
@@ -29,8 +37,11 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
                          hipStream_t st);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st);
+// Marks the record of every queued path pending (w = 1): k_splat skips it.
+hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st);
+// Completes every queued path and splats its sample into `film` itself.
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
-                         uint32_t G, int stack, hipStream_t st);
+                         const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 

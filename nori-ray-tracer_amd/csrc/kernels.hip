@@ -238,46 +238,80 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 
     else hits[q] = make_float4(t, __uint_as_float(p), u, v);
 }
 
-// Extension rays: closest hit of every queued path (two blocks per segment).
+// Trace work-groups are dealt out over groups of kTraceGroup consecutive
+// segments: the queue entries of a group are numbered through a prefix over
+// its segment counts and work-group j of the group takes entries
+// [128j, 128j+128).  Partly filled segments (a segment's shadow queue is about
+// half full; the drain phase empties them) therefore do not leave waves
+// partly idle, and every thread still traces one ray (short-lived waves keep
+// the kernel's tail short).
+struct SegRange {
+    uint32_t pre[kTraceGroup + 1];
+    uint32_t s0;
+};
+constexpr uint32_t kTraceSlices = kTraceGroup * kSeg / kTraceBlock;  // work-groups per group
+ND SegRange seg_range(const uint32_t *cnt, uint32_t G) {
+    SegRange r;
+    r.s0 = (blockIdx.x / kTraceSlices) * kTraceGroup;
+    r.pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
+    return r;
+}
+ND uint32_t seg_entry(const SegRange &r, uint32_t i) {
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 1; j < kTraceGroup; ++j) k += i >= r.pre[j] ? 1u : 0u;
+    uint32_t base = r.pre[0];
+#pragma unroll
+    for (int j = 1; j < kTraceGroup; ++j) base = k == (uint32_t)j ? r.pre[j] : base;
+    return (r.s0 + k) * kSeg + (i - base);
+}
+
+// Extension rays: closest hit of every queued path.
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt) {
+__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
     __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
-    const uint32_t seg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
-    if (idx >= cnt[seg]) return;
-    const uint32_t q = seg * kSeg + idx;
-    float4 a = pq.ray_o[q], b = pq.ray_d[q];
-    TRay r;
-    r.o = ld3(a);
-    r.d = ld3(b);
-    r.mint = a.w;
-    r.maxt = b.w;
-    float t, u, v;
-    uint32_t p;
-    traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
-    pq.hit[q] = make_float4(t, __uint_as_float(p), u, v);
+    const SegRange sr = seg_range(cnt, G);
+    const uint32_t i = (blockIdx.x % kTraceSlices) * kTraceBlock + threadIdx.x;
+    if (i < sr.pre[kTraceGroup]) {
+        const uint32_t q = seg_entry(sr, i);
+        float4 a = pq.ray_o[q], b = pq.ray_d[q];
+        TRay r;
+        r.o = ld3(a);
+        r.d = ld3(b);
+        r.mint = a.w;
+        r.maxt = b.w;
+        float t, u, v;
+        uint32_t p;
+        traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
+        pq.hit[q] = make_float4(t, __uint_as_float(p), u, v);
+    }
 }
 
 // Shadow rays: any hit; unoccluded -> record += payload.
 template <int STACK>
 __global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
-                                                        float4 *rec) {
+                                                        float4 *rec, uint32_t G) {
     __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
-    const uint32_t seg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
-    if (idx >= shcnt[seg]) return;
-    const uint32_t q = seg * kSeg + idx;
-    float4 a = sq.ray_o[q], b = sq.ray_d[q];
-    TRay r;
-    r.o = ld3(a);
-    r.d = ld3(b);
-    r.mint = a.w;
-    r.maxt = b.w;
-    float t, u, v;
-    uint32_t p;
-    if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) {
-        float4 c = sq.payload[q];
-        uint32_t w = __float_as_uint(c.w);
-        float4 L = rec[w];
-        rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, 0.0f);
+    const SegRange sr = seg_range(shcnt, G);
+    const uint32_t i = (blockIdx.x % kTraceSlices) * kTraceBlock + threadIdx.x;
+    if (i < sr.pre[kTraceGroup]) {
+        const uint32_t q = seg_entry(sr, i);
+        float4 a = sq.ray_o[q], b = sq.ray_d[q];
+        TRay r;
+        r.o = ld3(a);
+        r.d = ld3(b);
+        r.mint = a.w;
+        r.maxt = b.w;
+        float t, u, v;
+        uint32_t p;
+        if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) {
+            float4 c = sq.payload[q];
+            uint32_t w = __float_as_uint(c.w);
+            float4 L = rec[w];
+            rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
+        }
     }
 }
 
@@ -438,7 +472,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
             Ladd = ps.beta * Le;
         }
         float4 L = rec[ps.work];
-        rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, 0.0f);
+        rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, L.w);
     }
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
         float ul = next1D(ps.rng);
@@ -509,21 +543,36 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, PathState 
     rec[w] = make_float4(0, 0, 0, 0);
 }
 
+#ifndef NORI_SHADE_WAVES
+#define NORI_SHADE_WAVES 6
+#endif
+// lds_bytes != 0: the scene blob is staged into LDS first, so the chains of
+// dependent table reads of a vertex (shape -> bsdf -> vertices -> light CDF)
+// run at LDS instead of L2 latency.
 template <int INTEG>
-__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathQueue in, PathQueue out, ShadowQueue sq,
-                                                       SegState seg, int in_sel, WorkDesc wd, float4 *rec,
-                                                       Counters *C) {
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
+void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
+             float4 *rec, Counters *C, uint32_t lds_bytes) {
     __shared__ uint32_t s_need[kShadeBlock / 64], s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64];
+    extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, q = b * kSeg + tid;
     const uint32_t n_in = seg.cnt[in_sel][b];
     PathState ps;
+    float4 hit;
+    if (tid < n_in) {  // path loads in flight while the blob is staged
+        load_path(in, q, ps);
+        hit = in.hit[q];
+    }
+    DevScene S = Sg;
+    if (lds_bytes) {
+        for (uint32_t i = tid; i < lds_bytes / 16; i += kShadeBlock) blob_lds[i] = Sg.blob[i];
+        __syncthreads();
+        S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
+    }
     ShadowOut so;
     so.emit = false;
     bool alive = false;
-    if (tid < n_in) {
-        load_path(in, q, ps);
-        alive = shade_vertex<INTEG>(S, ps, in.hit[q], rec, so);
-    }
+    if (tid < n_in) alive = shade_vertex<INTEG>(S, ps, hit, rec, so);
     // ---- regenerate from this segment's work stream
     const bool need = !alive;
     const uint64_t mneed = __ballot(need), msh = __ballot(so.emit);
@@ -584,9 +633,46 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathQueue in,
 // Runs every path still queued to completion, one thread per path: the
 // Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
 // bounce) would otherwise cost three launches per bounce.
+// ImageBlock::put(pos, val) (block.cpp:93-122) of one sample straight into
+// the film, with the block-relative coordinates of the sample's own block so
+// the filter weights round exactly as in k_splat.
+ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, uint32_t y, V2 jit, float4 L) {
+    if (L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z)) {
+        atomicAdd(&C->invalid, 1ull);
+        return;
+    }
+    const int B = S.border, TS = NORI_BLOCK_SIZE + 2 * B, FW = S.W + 2 * B;
+    const int ox = (int)(x / NORI_BLOCK_SIZE) * NORI_BLOCK_SIZE, oy = (int)(y / NORI_BLOCK_SIZE) * NORI_BLOCK_SIZE;
+    const float rad = S.filter_radius, lk = S.lookup;
+    float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
+    int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
+    int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
+    for (int cy = y0; cy <= y1; ++cy) {
+        float wy = S.filter[min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION)];
+        for (int cx = x0; cx <= x1; ++cx) {
+            float wx = S.filter[min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION)];
+            float *f = film + 4 * ((size_t)(oy + cy) * FW + (ox + cx));
+            float a = (L.x * wx) * wy, b = (L.y * wx) * wy, c = (L.z * wx) * wy, w = (1.0f * wx) * wy;
+            if (w != 0.0f || a != 0.0f || b != 0.0f || c != 0.0f) {
+                atomicAdd(f + 0, a);
+                atomicAdd(f + 1, b);
+                atomicAdd(f + 2, c);
+                atomicAdd(f + 3, w);
+            }
+        }
+    }
+}
+
+// Pending marker for the samples the finisher will splat itself.
+__global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg, int sel, float4 *rec) {
+    const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
+    if (idx >= seg.cnt[sel][sg]) return;
+    rec[Q.work[sg * kSeg + idx]].w = 1.0f;
+}
+
 template <int STACK, int INTEG>
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
-                                                        float4 *rec) {
+                                                        float4 *rec, WorkDesc wd, float *film, Counters *C) {
     __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
@@ -617,7 +703,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             ++rays;
             if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) {
                 float4 L = rec[so.work];
-                rec[so.work] = make_float4(L.x + so.contrib.x, L.y + so.contrib.y, L.z + so.contrib.z, 0.0f);
+                rec[so.work] = make_float4(L.x + so.contrib.x, L.y + so.contrib.y, L.z + so.contrib.z, L.w);
             }
         }
         if (!alive) break;
@@ -629,6 +715,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         h = make_float4(t, __uint_as_float(p), u, v);
     }
     atomicAdd(&seg.stats[sg].w, rays);
+    // the sample is complete: splat it (k_splat skipped it as pending)
+    const uint32_t w = ps.work, pass = w / wd.M, e = w - pass * wd.M, pix = wd.pixels[e];
+    const uint32_t y = pix / (uint32_t)S.W, x = pix - y * (uint32_t)S.W;
+    Pcg r;
+    wave_seed(r, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
+    V2 jit = next2D(r);
+    splat_sample(S, film, C, x, y, jit, rec[w]);
 }
 
 // ------------------------------------------------------------------ film splat
@@ -665,6 +758,7 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
         bool any = false;
         for (uint32_t p = p0; p < p1; ++p) {
             float4 L = rec[(size_t)p * sd.M + off + j];
+            if (L.w != 0.0f) continue;  // pending: the finisher splats this sample
             uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
             Pcg r;
             wave_seed(r, sd.seed, sid);
@@ -754,57 +848,65 @@ hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue 
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                         hipStream_t st) {
     dim3 g(wd.G), b(kShadeBlock);
+    const uint32_t lds = S.blob_bytes <= kShadeLdsMax ? S.blob_bytes : 0u;
     if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C);
+        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C,
+                           lds);
     else
-        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C);
+        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C,
+                           lds);
     return hipGetLastError();
 }
 
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
-    dim3 g(2 * G), b(kTraceBlock);
+    dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     switch (stack) {
-    case 0: hipLaunchKernelGGL(k_extend<0>, g, b, 0, st, S, q, cnt); break;
-    case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt); break;
-    case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, cnt); break;
-    case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, cnt); break;
-    default: hipLaunchKernelGGL(k_extend<64>, g, b, 0, st, S, q, cnt); break;
+    case 0: hipLaunchKernelGGL(k_extend<0>, g, b, 0, st, S, q, cnt, G); break;
+    case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt, G); break;
+    case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, cnt, G); break;
+    case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, cnt, G); break;
+    default: hipLaunchKernelGGL(k_extend<64>, g, b, 0, st, S, q, cnt, G); break;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st) {
-    dim3 g(2 * G), b(kTraceBlock);
+    dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     switch (stack) {
-    case 0: hipLaunchKernelGGL(k_shadow<0>, g, b, 0, st, S, sq, shcnt, rec); break;
-    case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec); break;
-    case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec); break;
-    case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec); break;
-    default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec); break;
+    case 0: hipLaunchKernelGGL(k_shadow<0>, g, b, 0, st, S, sq, shcnt, rec, G); break;
+    case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec, G); break;
+    case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec, G); break;
+    case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec, G); break;
+    default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st) {
+    hipLaunchKernelGGL(k_mark, dim3(2 * G), dim3(kTraceBlock), 0, st, Q, seg, sel, rec);
     return hipGetLastError();
 }
 
 template <int INTEG>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
-                            uint32_t G, int stack, hipStream_t st) {
+                            const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st) {
     dim3 g(2 * G), b(kTraceBlock);
     switch (stack) {
-    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec); break;
+    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
     }
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
-                         uint32_t G, int stack, hipStream_t st) {
+                         const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st) {
     if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, G, stack, st);
+        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
     else
-        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, G, stack, st);
+        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
     return hipGetLastError();
 }
 

@@ -133,6 +133,8 @@ struct nori_scene {
 struct nori_gpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;       // film splat, overlapped with the tail finisher
+    hipEvent_t fork = nullptr, join = nullptr;
     DevScene S{};
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, blob;
@@ -151,6 +153,9 @@ struct nori_gpu_ctx {
     ~nori_gpu_ctx() {
         for (auto e : ring) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -440,6 +445,11 @@ struct Timers {
     }
 };
 
+bool overlap_splat() {
+    const char *e = std::getenv("NORI_SPLAT_OVERLAP");
+    return !(e && e[0] == '0');
+}
+
 int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nori_gpu_stats *stats) {
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(c.device));
@@ -515,17 +525,18 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     };
     std::vector<Span> spans;
     const bool timing = rd.timing != 0;
-    auto timed = [&](int kind, auto &&launch) {
+    auto timed_on = [&](hipStream_t st, int kind, auto &&launch) {
         if (!timing) {
             HIP_TRY(launch());
             return;
         }
         Span s{tm.get(), tm.get(), kind};
-        HIP_TRY(hipEventRecord(s.a, c.stream));
+        HIP_TRY(hipEventRecord(s.a, st));
         HIP_TRY(launch());
-        HIP_TRY(hipEventRecord(s.b, c.stream));
+        HIP_TRY(hipEventRecord(s.b, st));
         spans.push_back(s);
     };
+    auto timed = [&](int kind, auto &&launch) { timed_on(c.stream, kind, launch); };
     bool cancelled = false;
     const uint32_t G = pool / kSeg;
     SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
@@ -534,7 +545,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     uint64_t finish_rays = 0, samples_started = 0;
     for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
         uint32_t np = std::min(chunk, passes - p0);
-        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev};
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev, 1};
+        wd.rot = stream_rotation(wd.total, M, G);
         __atomic_store_n(&c.pinned[0], 0u, __ATOMIC_RELEASE);
         __atomic_store_n(&c.pinned[1], 0u, __ATOMIC_RELEASE);
         // segments whose stream is empty from the start count as exhausted
@@ -569,10 +581,23 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             }
         }
         if (cancelled) break;
-        timed(4, [&] { return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.bvh_stack, c.stream); });
+        // The samples still in flight are marked pending; the film splat of all
+        // the others runs on the side stream while the finisher completes the
+        // pending ones and splats each itself.
+        // (NORI_SPLAT_OVERLAP=0: splat after the finisher on the same stream.)
+        const bool overlap = overlap_splat();
+        hipStream_t splat_st = overlap ? c.side : c.stream;
+        HIP_TRY(launch_mark(Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stream));
+        HIP_TRY(hipEventRecord(c.fork, c.stream));
+        HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)),
                      c.blocks.as<int4>(), rd.seed};
-        timed(3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream); });
+        timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
+        timed(4, [&] {
+            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.bvh_stack, c.stream);
+        });
+        HIP_TRY(hipEventRecord(c.join, c.side));
+        HIP_TRY(hipStreamWaitEvent(c.stream, c.join, 0));
         Counters hc;
         HIP_TRY(hipMemcpyAsync(&hc, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
         HIP_TRY(hipMemcpyAsync(hstats.data(), seg.stats, 16 * (size_t)G, hipMemcpyDeviceToHost, c.stream));
@@ -686,6 +711,9 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         std::unique_ptr<nori_gpu_ctx> c(new nori_gpu_ctx);
         c->device = device;
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         upload_scene(*c, *d);
         *out = c.release();
         return NORI_OK;

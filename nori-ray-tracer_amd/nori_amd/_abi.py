@@ -115,7 +115,8 @@ SIGNATURES = {
 }
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libnori_gpu.so")
+# NORI_GPU_LIB: another in-tree build of the library (tuning variants under lib/)
+LIB_PATH = os.environ.get("NORI_GPU_LIB") or os.path.join(PKG_DIR, "lib", "libnori_gpu.so")
 
 _lib = None
 
