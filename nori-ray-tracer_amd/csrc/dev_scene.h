@@ -50,6 +50,7 @@ struct DevScene {
     uint32_t num_emitters;
     uint32_t num_nodes;
     uint32_t num_prims;
+    uint32_t num_scan_tris;  // scan mode: prims = triangles (padded to kScanGroup), then spheres
     float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;
     float invW, invH;
@@ -109,6 +110,7 @@ struct ShadowQueue {
 // static stream of 256-id chunks (consecutive ids = adjacent pixels of one
 // 32x32 block, so a segment traces coherent camera rays).
 constexpr uint32_t kSeg = 256;
+constexpr uint32_t kScanGroup = 4;  // triangles fetched per batch of scalar loads in the scan
 struct WorkDesc {
     uint64_t total;          // work ids in this chunk of passes
     uint32_t M;              // pixels in the selected blocks
@@ -149,6 +151,9 @@ struct Counters {
     uint32_t pad0[31];
     unsigned long long invalid;    // dropped samples (splat)
     unsigned long long pad1[15];
+    uint32_t finish_paths;         // paths completed by the tail finisher
+    uint32_t finish_max_rays;      // most rays traced by one finisher path
+    uint32_t pad2[30];
 };
 
 }  // namespace nori

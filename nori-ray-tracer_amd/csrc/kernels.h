@@ -13,6 +13,10 @@ constexpr int kTraceBlock = 128;   // traversal work-group size (LDS stack colum
 #endif
 constexpr int kTraceGroup = NORI_TRACE_GROUP;  // segments per extend/shadow work-group
 constexpr int kSplatBlock = 256;
+#ifndef NORI_SCAN_RAYS
+#define NORI_SCAN_RAYS 2
+#endif
+constexpr int kScanRays = NORI_SCAN_RAYS;  // rays per thread of the scan-mode trace kernels
 #ifndef NORI_SHADE_LDS_MAX
 #define NORI_SHADE_LDS_MAX 16384
 #endif
@@ -30,8 +34,10 @@ struct SplatDesc {
 // stack = LDS stack depth (8, 16, 32 or 64) chosen from the BVH depth.
 hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int any_hit, float4 *hits, int stack,
                         hipStream_t st);
+// trace: also find the closest hit of every outgoing ray (scan-mode scenes;
+// launch_extend is then skipped).
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
+                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                         hipStream_t st);
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st);

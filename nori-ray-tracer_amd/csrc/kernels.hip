@@ -120,52 +120,112 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
     return (disc > 0) && (h1 || h2);
 }
 
+// Small scenes: wave-uniform scan of the primitive list.  Every lane tests
+// every primitive in the same order, so the records arrive through scalar
+// loads and no lane diverges; the result is the closest hit (ties: last
+// primitive in scan order wins, as with the reference's `t <= maxt` update,
+// mesh.cpp:119).  The list holds the triangles first, padded with
+// never-hit records to a multiple of kScanGroup so that each group's records
+// come in one batch of scalar loads, then the spheres.  The root box test of
+// bvh.cpp:420 is kept so rays missing the scene never report hits.  K rays
+// per thread share every fetched record.  Expects the adaptive epsilon and
+// rcp already applied by the caller (scan_prologue).
+template <int K>
+ND void scan_prologue(const DevScene &S, TRay (&r)[K], bool (&live)[K]) {
+    const float4 rmn = make_float4(S.root_min[0], S.root_min[1], S.root_min[2], 0.f);
+    const float4 rmx = make_float4(S.root_max[0], S.root_max[1], S.root_max[2], 0.f);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        TRay &x = r[k];
+        if (x.mint == kEps) x.mint = smax(x.mint, x.mint * smax(smax(fabsf(x.o.x), fabsf(x.o.y)), fabsf(x.o.z)));
+        x.rcp = V3{1.0f / x.d.x, 1.0f / x.d.y, 1.0f / x.d.z};
+        float tn;
+        live[k] = live[k] && !(x.maxt < x.mint) && box_test(rmn, rmx, x, tn);
+    }
+}
+template <int K, bool ANY>
+ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
+                  float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
+    scan_prologue<K>(S, r, live);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        tb[k] = INF_F;
+        pb[k] = 0xFFFFFFFFu;
+        ub[k] = vb[k] = 0.0f;
+        found[k] = false;
+    }
+    auto all_done = [&]() {
+        bool done = true;
+#pragma unroll
+        for (int k = 0; k < K; ++k) done = done && (found[k] || !live[k]);
+        return __all(done);
+    };
+    const uint32_t nt = S.num_scan_tris, n = S.num_prims;
+    for (uint32_t i = 0; i < nt; i += kScanGroup) {
+        if (ANY && all_done()) return;
+        const float4 *p = S.prims + 3 * (size_t)i;
+        float4 q[3 * kScanGroup];
+#pragma unroll
+        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) q[j] = p[j];
+#pragma unroll
+        for (uint32_t g = 0; g < kScanGroup; ++g) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                float t = 0, u = 0, v = 0;
+                bool h = tri_hit_nb(q[3 * g], q[3 * g + 1], q[3 * g + 2], r[k], t, u, v);
+                if (h && live[k]) {
+                    found[k] = true;
+                    if (!ANY) {
+                        r[k].maxt = tb[k] = t;
+                        ub[k] = u;
+                        vb[k] = v;
+                        pb[k] = __float_as_uint(q[3 * g].w);
+                    }
+                }
+            }
+        }
+    }
+    for (uint32_t i = nt; i < n; ++i) {
+        if (ANY && all_done()) return;
+        const float4 *p = S.prims + 3 * (size_t)i;
+        float4 p0 = p[0], p1 = p[1];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float t = 0;
+            bool h = sphere_hit_nb(p0, p1, r[k], t);
+            if (h && live[k]) {
+                found[k] = true;
+                if (!ANY) {
+                    r[k].maxt = tb[k] = t;
+                    ub[k] = vb[k] = 0.0f;
+                    pb[k] = __float_as_uint(p0.w);
+                }
+            }
+        }
+    }
+}
+
 // BVH::rayIntersect (bvh.cpp:404-462): adaptive epsilon, closest or any hit.
 // Near child first; the short stack lives in LDS, one column per lane.
 template <int STACK, bool ANY>
 ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &pb, float &ub, float &vb) {
+    if constexpr (STACK == 0) {
+        TRay rr[1] = {r};
+        bool live[1] = {true}, found[1];
+        float t1[1], u1[1], v1[1];
+        uint32_t p1[1];
+        scan_core<1, ANY>(S, rr, live, t1, p1, u1, v1, found);
+        tb = t1[0];
+        pb = p1[0];
+        ub = u1[0];
+        vb = v1[0];
+        return found[0];
+    }
     if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
     tb = INF_F;
     pb = 0xFFFFFFFFu;
     ub = vb = 0.0f;
     r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
-    if constexpr (STACK == 0) {
-        // Small scenes: wave-uniform scan of the primitive list.  Every lane
-        // tests every primitive in the same order, so the records arrive
-        // through scalar loads and no lane diverges; the result is the
-        // closest hit (ties: last primitive wins, as with the reference's
-        // `t <= maxt` update, mesh.cpp:119).  The root box test of
-        // bvh.cpp:420 is kept so rays missing the scene never report hits.
-        const float4 rmn = make_float4(S.root_min[0], S.root_min[1], S.root_min[2], 0.f);
-        const float4 rmx = make_float4(S.root_max[0], S.root_max[1], S.root_max[2], 0.f);
-        float tn;
-        bool live = !(r.maxt < r.mint) && box_test(rmn, rmx, r, tn);
-        bool found = false;
-        const uint32_t n = S.num_prims;
-        auto test = [&](uint32_t i) {
-            const float4 *p = S.prims + 3 * (size_t)i;
-            float4 p0 = p[0], p1 = p[1], p2 = p[2];
-            float t = 0, u = 0, v = 0;
-            bool tri = __float_as_uint(p1.w) == 0u;
-            bool h = tri ? tri_hit_nb(p0, p1, p2, r, t, u, v) : sphere_hit_nb(p0, p1, r, t);
-            if (h && live) {
-                found = true;
-                if (!ANY) {
-                    r.maxt = tb = t;
-                    ub = tri ? u : 0.0f;
-                    vb = tri ? v : 0.0f;
-                    pb = __float_as_uint(p0.w);
-                }
-            }
-        };
-        if constexpr (ANY) {
-            for (uint32_t i = 0; i < n && !__all(found || !live); ++i) test(i);
-        } else {
-#pragma unroll 2
-            for (uint32_t i = 0; i < n; ++i) test(i);
-        }
-        return found;
-    }
     if (r.maxt < r.mint) return false;
     uint32_t ref = 0;
     int sp = 0;
@@ -258,6 +318,14 @@ ND SegRange seg_range(const uint32_t *cnt, uint32_t G) {
     for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
     return r;
 }
+ND SegRange seg_range_k(const uint32_t *cnt, uint32_t G, uint32_t K) {
+    SegRange r;
+    r.s0 = (blockIdx.x / (kTraceSlices / K)) * kTraceGroup;
+    r.pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
+    return r;
+}
 ND uint32_t seg_entry(const SegRange &r, uint32_t i) {
     uint32_t k = 0;
 #pragma unroll
@@ -313,6 +381,81 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue 
             rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
         }
     }
+}
+
+// Scan-mode traversal of K rays per thread: every primitive record is
+// fetched once (scalar loads) and tested against K independent rays, which
+// gives the VALU K independent dependency chains to interleave.  Results are
+// those of traverse<0, ANY> ray by ray.
+template <int K, bool ANY>
+ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
+                  float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
+    scan_core<K, ANY>(S, r, live, tb, pb, ub, vb, found);
+}
+
+template <int K>
+__global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
+                                                             uint32_t G) {
+    const SegRange sr = seg_range_k(cnt, G, K);
+    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
+    TRay r[K];
+    bool live[K];
+    uint32_t q[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t i = i0 + k * kTraceBlock;
+        live[k] = i < n;
+        q[k] = live[k] ? seg_entry(sr, i) : 0u;
+        float4 a = live[k] ? pq.ray_o[q[k]] : make_float4(0, 0, 0, 0);
+        float4 b = live[k] ? pq.ray_d[q[k]] : make_float4(0, 0, 1, 0);
+        r[k].o = ld3(a);
+        r[k].d = ld3(b);
+        r[k].mint = a.w;
+        r[k].maxt = b.w;
+    }
+    if (!live[0]) return;  // entries fill the slice from its start
+    float t[K], u[K], v[K];
+    uint32_t p[K];
+    bool f[K];
+    scan_rays<K, false>(S, r, live, t, p, u, v, f);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (i0 + k * kTraceBlock < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
+}
+
+template <int K>
+__global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
+                                                             float4 *rec, uint32_t G) {
+    const SegRange sr = seg_range_k(shcnt, G, K);
+    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
+    TRay r[K];
+    bool live[K], valid[K];
+    uint32_t q[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t i = i0 + k * kTraceBlock;
+        valid[k] = live[k] = i < n;
+        q[k] = live[k] ? seg_entry(sr, i) : 0u;
+        float4 a = live[k] ? sq.ray_o[q[k]] : make_float4(0, 0, 0, 0);
+        float4 b = live[k] ? sq.ray_d[q[k]] : make_float4(0, 0, 1, 0);
+        r[k].o = ld3(a);
+        r[k].d = ld3(b);
+        r[k].mint = a.w;
+        r[k].maxt = b.w;
+    }
+    if (!valid[0]) return;
+    float t[K], u[K], v[K];
+    uint32_t p[K];
+    bool f[K];
+    scan_rays<K, true>(S, r, live, t, p, u, v, f);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (valid[k] && !f[k]) {
+            float4 c = sq.payload[q[k]];
+            uint32_t w = __float_as_uint(c.w);
+            float4 L = rec[w];
+            rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
+        }
 }
 
 // ------------------------------------------------------------------ shading helpers
@@ -549,7 +692,10 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, PathState 
 // lds_bytes != 0: the scene blob is staged into LDS first, so the chains of
 // dependent table reads of a vertex (shape -> bsdf -> vertices -> light CDF)
 // run at LDS instead of L2 latency.
-template <int INTEG>
+// TRACE (scan-mode scenes): the closest hit of every outgoing ray is found
+// here as well (wave-uniform scan, traverse<0>), so the rays do not make a
+// round trip through HBM to a separate extension kernel.
+template <int INTEG, bool TRACE>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
@@ -612,6 +758,15 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         al_tot += s_al[w] & 0xFFFFu;
         fresh_tot += s_al[w] >> 16;
     }
+    if (TRACE) {
+        TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
+        if (!alive) r.maxt = -1.0f;  // lane takes part in the scan without a ray
+        float t, u, v;
+        uint32_t p;
+        uint32_t *no_stack = nullptr;
+        traverse<0, false>(Sg, r, no_stack, t, p, u, v);
+        if (alive) out.hit[b * kSeg + al_off] = make_float4(t, __uint_as_float(p), u, v);
+    }
     if (alive) store_path(out, b * kSeg + al_off, ps);
     if (tid == 0) {
         seg.cnt[in_sel ^ 1][b] = al_tot;
@@ -630,9 +785,6 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     }
 }
 
-// Runs every path still queued to completion, one thread per path: the
-// Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
-// bounce) would otherwise cost three launches per bounce.
 // ImageBlock::put(pos, val) (block.cpp:93-122) of one sample straight into
 // the film, with the block-relative coordinates of the sample's own block so
 // the filter weights round exactly as in k_splat.
@@ -670,6 +822,89 @@ __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg,
     rec[Q.work[sg * kSeg + idx]].w = 1.0f;
 }
 
+// Cooperative scan (scan-mode scenes, n <= 64 primitives): the rays of the
+// lanes in `want` are traced one after another by the whole wave, lane l
+// testing primitive l against the broadcast ray, then a wave reduction.  The
+// result is exactly that of traverse<0, ANY> for the ray: every candidate
+// passes the test against the ray's own maxt, the closest wins, and among
+// equal t the last primitive in scan order wins (the `t <= maxt` update).
+// A lone tail path then pays one primitive test per ray instead of n.
+template <bool ANY>
+ND bool coop_scan(const DevScene &S, const TRay &mine, bool want, float &t, uint32_t &p, float &u, float &v) {
+    const uint32_t lane = lane_id();
+    const bool has = lane < S.num_prims;
+    float4 p0 = make_float4(0, 0, 0, 0), p1 = p0, p2 = p0;
+    if (has) {
+        const float4 *pp = S.prims + 3 * (size_t)lane;
+        p0 = pp[0];
+        p1 = pp[1];
+        p2 = pp[2];
+    }
+    const bool tri = __float_as_uint(p1.w) == 0u;
+    const float4 rmn = make_float4(S.root_min[0], S.root_min[1], S.root_min[2], 0.f);
+    const float4 rmx = make_float4(S.root_max[0], S.root_max[1], S.root_max[2], 0.f);
+    bool res = false;
+    t = INF_F;
+    p = 0xFFFFFFFFu;
+    u = v = 0.0f;
+    auto bcast = [](float x, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j)); };
+    uint64_t m = __ballot(want);
+    while (m) {
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        TRay r;
+        r.o = V3{bcast(mine.o.x, j), bcast(mine.o.y, j), bcast(mine.o.z, j)};
+        r.d = V3{bcast(mine.d.x, j), bcast(mine.d.y, j), bcast(mine.d.z, j)};
+        r.mint = bcast(mine.mint, j);
+        r.maxt = bcast(mine.maxt, j);
+        if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
+        r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+        float tn;
+        const bool live = !(r.maxt < r.mint) && box_test(rmn, rmx, r, tn);
+        float tl = 0, ul = 0, vl = 0;
+        bool hl = false;
+        if (has) hl = tri ? tri_hit_nb(p0, p1, p2, r, tl, ul, vl) : sphere_hit_nb(p0, p1, r, tl);
+        hl = hl && live;
+        if (ANY) {
+            const bool any = __ballot(hl) != 0ull;
+            if ((int)lane == j) res = any;
+        } else {
+            // key: t (positive, so its bits order like the value), then the
+            // highest lane among equal t
+            uint32_t khi = hl ? __float_as_uint(tl + 0.0f) : 0xFFFFFFFFu, klo = hl ? 63u - lane : 0xFFFFFFFFu;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                uint32_t ohi = (uint32_t)__shfl_xor((int)khi, o), olo = (uint32_t)__shfl_xor((int)klo, o);
+                bool take = ohi < khi || (ohi == khi && olo < klo);
+                khi = take ? ohi : khi;
+                klo = take ? olo : klo;
+            }
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(klo);
+            if (lo != 0xFFFFFFFFu) {
+                const int w = 63 - (int)lo;
+                const float tw = bcast(tl, w), uw = bcast(tri ? ul : 0.0f, w), vw = bcast(tri ? vl : 0.0f, w);
+                const uint32_t pw = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(p0.w), w);
+                if ((int)lane == j) {
+                    res = true;
+                    t = tw;
+                    p = pw;
+                    u = uw;
+                    v = vw;
+                }
+            }
+        }
+    }
+    return res;
+}
+
+// At most this many tracing lanes use the cooperative scan (each costs one
+// primitive test per lane and a reduction; the per-lane scan costs n tests).
+constexpr int kCoopMax = 4;
+
+// Runs every path still queued to completion, one thread per path: the
+// Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
+// bounce) would otherwise cost three launches per bounce.  Waves loop while
+// any lane's path is alive so that the lanes can trace cooperatively.
 template <int STACK, int INTEG>
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C) {
@@ -687,41 +922,59 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
     }
-    if (idx >= n) return;
+    if ((idx & ~63u) >= n) return;  // whole wave idle
     const uint32_t q = sg * kSeg + idx;
+    bool active = idx < n;
     PathState ps;
-    load_path(Q, q, ps);
-    float4 h = Q.hit[q];
+    float4 h = make_float4(0, 0, 0, 0);
+    if (active) {
+        load_path(Q, q, ps);
+        h = Q.hit[q];
+    }
     uint32_t rays = 0;
-    for (;;) {
+    auto trace = [&](const TRay &r, bool want, bool any_hit, float &t, uint32_t &p, float &u, float &v) -> bool {
+        if (STACK == 0 && S.num_prims <= 64 && __popcll(__ballot(want)) <= kCoopMax)
+            return any_hit ? coop_scan<true>(S, r, want, t, p, u, v) : coop_scan<false>(S, r, want, t, p, u, v);
+        if (!want) return false;
+        return any_hit ? traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)
+                       : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
+    };
+    while (__ballot(active)) {
         ShadowOut so;
-        bool alive = shade_vertex<INTEG>(S, ps, h, rec, so);
-        if (so.emit) {
+        so.emit = false;
+        bool alive = false;
+        if (active) alive = shade_vertex<INTEG>(S, ps, h, rec, so);
+        {
             TRay r{so.o, so.d, V3{0, 0, 0}, kEps, so.maxt};
             float t, u, v;
             uint32_t p;
-            ++rays;
-            if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) {
+            rays += so.emit ? 1u : 0u;
+            bool occluded = trace(r, so.emit, true, t, p, u, v);
+            if (so.emit && !occluded) {
                 float4 L = rec[so.work];
                 rec[so.work] = make_float4(L.x + so.contrib.x, L.y + so.contrib.y, L.z + so.contrib.z, L.w);
             }
         }
-        if (!alive) break;
+        if (active && !alive) {
+            active = false;
+            // the sample is complete: splat it (k_splat skipped it as pending)
+            const uint32_t w = ps.work, pass = w / wd.M, e = w - pass * wd.M, pix = wd.pixels[e];
+            const uint32_t y = pix / (uint32_t)S.W, x = pix - y * (uint32_t)S.W;
+            Pcg rg;
+            wave_seed(rg, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
+            V2 jit = next2D(rg);
+            splat_sample(Sg, film, C, x, y, jit, rec[w]);  // Sg: kernarg filter table (no local copy)
+            atomicAdd(&seg.stats[sg].w, rays);
+            atomicAdd(&C->finish_paths, 1u);
+            atomicMax(&C->finish_max_rays, rays);
+        }
         TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
         float t, u, v;
         uint32_t p;
-        ++rays;
-        traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
-        h = make_float4(t, __uint_as_float(p), u, v);
+        rays += active ? 1u : 0u;
+        trace(r, active, false, t, p, u, v);
+        if (active) h = make_float4(t, __uint_as_float(p), u, v);
     }
-    atomicAdd(&seg.stats[sg].w, rays);
-    // the sample is complete: splat it (k_splat skipped it as pending)
-    const uint32_t w = ps.work, pass = w / wd.M, e = w - pass * wd.M, pix = wd.pixels[e];
-    const uint32_t y = pix / (uint32_t)S.W, x = pix - y * (uint32_t)S.W;
-    Pcg r;
-    wave_seed(r, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
-    V2 jit = next2D(r);
-    splat_sample(S, film, C, x, y, jit, rec[w]);
 }
 
 // ------------------------------------------------------------------ film splat
@@ -845,22 +1098,36 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 }
 
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
+                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                         hipStream_t st) {
     dim3 g(wd.G), b(kShadeBlock);
     const uint32_t lds = S.blob_bytes <= kShadeLdsMax ? S.blob_bytes : 0u;
-    if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C,
-                           lds);
-    else
-        hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C,
-                           lds);
+    if (trace) {
+        if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
+            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS, true>), g, b, lds, st, S, in, out, sq, seg, in_sel,
+                               wd, rec, C, lds);
+        else
+            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS, true>), g, b, lds, st, S, in, out, sq, seg, in_sel,
+                               wd, rec, C, lds);
+    } else {
+        if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
+            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS, false>), g, b, lds, st, S, in, out, sq, seg, in_sel,
+                               wd, rec, C, lds);
+        else
+            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS, false>), g, b, lds, st, S, in, out, sq, seg, in_sel,
+                               wd, rec, C, lds);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
+    if (stack == 0 && kScanRays > 1) {
+        dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
+        hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
+        return hipGetLastError();
+    }
     switch (stack) {
     case 0: hipLaunchKernelGGL(k_extend<0>, g, b, 0, st, S, q, cnt, G); break;
     case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt, G); break;
@@ -874,6 +1141,11 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
+    if (stack == 0 && kScanRays > 1) {
+        dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
+        hipLaunchKernelGGL(k_shadow_scan<kScanRays>, gk, b, 0, st, S, sq, shcnt, rec, G);
+        return hipGetLastError();
+    }
     switch (stack) {
     case 0: hipLaunchKernelGGL(k_shadow<0>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec, G); break;

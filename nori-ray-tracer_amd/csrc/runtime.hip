@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -139,7 +140,6 @@ struct nori_gpu_ctx {
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, blob;
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
-    int bvh_stack = 8;   // LDS stack depth of the BVH (tail finisher)
     uint32_t bvh_depth = 0, bvh_nodes = 0, num_prims = 0;
     size_t scene_bytes = 0;
     std::atomic<int> cancel{0};
@@ -307,8 +307,33 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     bool scan = off <= kScanMaxPrims;
     if (mode && std::string(mode) == "bvh") scan = false;
     if (mode && std::string(mode) == "scan") scan = true;
-    c.bvh_stack = c.stack;  // the tail finisher always walks the BVH: shorter critical path per lone lane
     if (scan) c.stack = 0;
+    // scan order: triangles (leaf order) padded to kScanGroup with records no
+    // ray hits (zero edges: det = 0, or NaN t), then spheres (leaf order)
+    std::vector<float> scan_prims;
+    uint32_t scan_tris = 0;
+    if (scan) {
+        auto is_sphere = [&](uint32_t i) {
+            uint32_t f;
+            std::memcpy(&f, &bvh.prims[12 * (size_t)i + 7], 4);
+            return f != 0u;
+        };
+        auto add = [&](uint32_t i) {
+            scan_prims.insert(scan_prims.end(), bvh.prims.begin() + 12 * (size_t)i, bvh.prims.begin() + 12 * (size_t)i + 12);
+        };
+        for (uint32_t i = 0; i < off; ++i)
+            if (!is_sphere(i)) add(i), ++scan_tris;
+        while (scan_tris % kScanGroup) {
+            float null_prim[12] = {0};
+            const uint32_t none = 0xFFFFFFFFu;
+            std::memcpy(&null_prim[3], &none, 4);
+            scan_prims.insert(scan_prims.end(), null_prim, null_prim + 12);
+            ++scan_tris;
+        }
+        for (uint32_t i = 0; i < off; ++i)
+            if (is_sphere(i)) add(i);
+    }
+    const std::vector<float> &prim_list = scan ? scan_prims : bvh.prims;
 
     std::vector<float> pos(4 * (size_t)d.num_vertices), nrm(4 * (size_t)d.num_vertices);
     for (uint32_t v = 0; v < d.num_vertices; ++v)
@@ -319,7 +344,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     if (pos.empty()) pos.assign(4, 0.0f), nrm.assign(4, 0.0f);
     if (cdf.empty()) cdf.assign(1, 0.0f);
     c.nodes.upload(bvh.nodes);
-    c.prims.upload(bvh.prims);
+    c.prims.upload(prim_list);
     c.tri_vidx.upload(tri_vidx);
     c.pos.upload(pos);
     c.nrm.upload(nrm);
@@ -338,7 +363,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         const char *b = static_cast<const char *>(p);
         blob.insert(blob.end(), b, b + n);
     };
-    put(0, bvh.prims.data(), bvh.prims.size() * 4);
+    put(0, prim_list.data(), prim_list.size() * 4);
     put(1, tri_vidx.data(), tri_vidx.size() * 4);
     put(2, pos.data(), pos.size() * 4);
     put(3, nrm.data(), nrm.size() * 4);
@@ -365,7 +390,8 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.cdf = c.cdf.as<float>();
     S.num_emitters = d.num_emitters;
     S.num_nodes = bvh.num_nodes;
-    S.num_prims = off;
+    S.num_prims = (uint32_t)(prim_list.size() / 12);
+    S.num_scan_tris = scan_tris;
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     S.blob = use_blob ? c.blob.as<float4>() : nullptr;
     S.blob_bytes = use_blob ? (uint32_t)blob.size() : 0u;
@@ -445,6 +471,14 @@ struct Timers {
     }
 };
 
+bool debug_log() {
+    const char *e = std::getenv("NORI_DEBUG");
+    return e && e[0] == '1';
+}
+bool fused_extend() {
+    const char *e = std::getenv("NORI_FUSED_EXTEND");
+    return e && e[0] == '1';
+}
 bool overlap_splat() {
     const char *e = std::getenv("NORI_SPLAT_OVERLAP");
     return !(e && e[0] == '0');
@@ -538,6 +572,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     };
     auto timed = [&](int kind, auto &&launch) { timed_on(c.stream, kind, launch); };
     bool cancelled = false;
+    // NORI_FUSED_EXTEND=1: scan-mode scenes trace the extension rays inside
+    // the shade kernel (measured even with separate k_extend launches)
+    const bool fused = c.stack == 0 && fused_extend();
     const uint32_t G = pool / kSeg;
     SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
                  c.segstats.as<uint4>()};
@@ -561,8 +598,10 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         for (uint64_t it = 0;; ++it) {
             int in = (int)(it & 1), out = in ^ 1;
             last_out = out;
-            timed(2, [&] { return launch_shade(S, Q[in], Q[out], sq, seg, in, wd, c.rec.as<float4>(), C, c.stream); });
-            timed(0, [&] { return launch_extend(S, Q[out], seg.cnt[out], G, c.stack, c.stream); });
+            timed(2, [&] {
+                return launch_shade(S, Q[in], Q[out], sq, seg, in, wd, c.rec.as<float4>(), C, fused, c.stream);
+            });
+            if (!fused) timed(0, [&] { return launch_extend(S, Q[out], seg.cnt[out], G, c.stack, c.stream); });
             timed(1, [&] { return launch_shadow(S, sq, seg.shcnt, c.rec.as<float4>(), G, c.stack, c.stream); });
             HIP_TRY(hipEventRecord(c.ring[it % kRing], c.stream));
             ++iters;
@@ -594,7 +633,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                      c.blocks.as<int4>(), rd.seed};
         timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
         timed(4, [&] {
-            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.bvh_stack, c.stream);
+            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack, c.stream);
         });
         HIP_TRY(hipEventRecord(c.join, c.side));
         HIP_TRY(hipStreamWaitEvent(c.stream, c.join, 0));
@@ -609,6 +648,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             finish_rays += st.w;
         }
         invalid += hc.invalid;
+        if (debug_log())
+            std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays\n", p0,
+                         (unsigned long)iters, hc.finish_paths, hc.finish_max_rays);
         done_before += wd.total;
     }
     if (samples_started != done_before && !cancelled)
