@@ -12,9 +12,13 @@ over RCCL (all_reduce) -- the reference's ImageBlock::put(block) merge
 (block.cpp:124-133).  value = samples of all ranks / max-over-ranks time.
 
 Extra fields:
-  roofline     -- extension-ray traversal kernel (k_extend), algorithmic bytes
-                  per launch (48 B per ray + BVH bytes) over its average
-                  HIP-event launch time, against 8 TB/s HBM peak.
+  roofline     -- the dominant kernel (most HIP-event time in the last timed
+                  step; k_shade on this workload): algorithmic HBM bytes per
+                  launch over its average launch time against the 8 TB/s HBM
+                  peak, `traffic` = measured HBM bytes per launch from the
+                  committed rocprofv3 PMC summary (profiles/pmc_r01.json), and
+                  a per-kernel table (the traversal kernels are VALU-bound:
+                  VALU issue rate against the issue peak).
   cpu_baseline -- the CPU oracle (reference structure: sample-outer passes,
                   32x32 blocks, per-block pcg32 streams) timed on this host on
                   a bounded sample of the same workload (rank 0, N=1 only).
@@ -83,14 +87,65 @@ def parity_check():
     return {"l2": float(np.mean((gpu - cpu) ** 2)), "config": "128x128@16spp, identical WAVE streams"}
 
 
-def load_traffic(stats):
-    """HBM bytes per k_extend launch from the committed rocprofv3 PMC pass, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_extend.json")
+PROFILE = os.path.join(ROOT, "profiles", "pmc_r01.json")  # committed rocprofv3 evidence (tools/pmc_to_profile.py)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2 * 64  # lane-instr/s: 256 CUs x 4 SIMDs, a wave64 VALU op per 2 cycles
+
+
+def profiled(prefix):
+    """Per-launch rocprofv3 numbers of the kernel whose name starts with `prefix`, if committed."""
     try:
-        d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch")
+        d = json.load(open(PROFILE))
     except (OSError, ValueError):
         return None
+    for k, v in d.get("kernels", {}).items():
+        if k.startswith(prefix):
+            return dict(v, name=k)
+    return None
+
+
+def roofline(ts, samples):
+    """Roofline of the dominant kernel (most HIP-event time) of the timing render.
+
+    Algorithmic HBM bytes per kernel:
+      k_shade : per path read ray_o, ray_d, thr, rng, hit (16 B each) + work (4 B) = 84 B,
+                per surviving path write ray_o, ray_d, thr, rng + work = 68 B,
+                per shadow ray 48 B (origin, direction, payload), per new sample 16 B
+                record + 4 B pixel index
+      k_extend: per ray read ray_o, ray_d (32 B), write hit (16 B)
+      k_shadow: per shadow ray read ray_o, ray_d, payload (48 B)
+    The traversal kernels are VALU-bound (scan over the primitive list); their
+    VALU issue rate (SQ_INSTS_VALU x 64 lanes per launch, rocprofv3) is given
+    against the issue peak.
+    """
+    launches = max(ts["iterations"], 1)
+    rc, rs = ts["rays_closest"], ts["rays_shadow"]
+    kern = {
+        "shade": ("k_shade", ts["ms_shade"], rc * (84 + 68) + rs * 48 + samples * 20),
+        "extend": ("k_extend", ts["ms_extend"], rc * 48),
+        "shadow": ("k_shadow", ts["ms_shadow"], rs * 48),
+    }
+    rows = {}
+    for key, (name, ms, nbytes) in kern.items():
+        if ms <= 0:
+            continue
+        prof = profiled(name)
+        avg = ms / launches
+        row = {"ms": ms, "avg_launch_ms": avg, "bytes_per_launch": nbytes / launches,
+               "achieved_GBs": nbytes / launches / (avg / 1e3) / 1e9}
+        if prof:
+            row["traffic_bytes_per_launch"] = prof.get("hbm_bytes_per_launch")
+            row["rocprof_avg_launch_ms"] = prof.get("trace_avg_ms")
+            if prof.get("sq_insts_valu_per_launch") and prof.get("trace_avg_ms"):
+                rate = prof["sq_insts_valu_per_launch"] * 64 / (prof["trace_avg_ms"] / 1e3)
+                row["valu_lane_instr_per_s"] = rate
+                row["valu_issue_frac"] = rate / VALU_PEAK
+        rows[name] = row
+    dom = max(rows, key=lambda k: rows[k]["ms"])
+    d = rows[dom]
+    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": d["achieved_GBs"] / HBM_PEAK_GBS, "traffic": d.get("traffic_bytes_per_launch"),
+            "bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": d["avg_launch_ms"], "launches": launches,
+            "kernels": rows}
 
 
 def main():
@@ -149,8 +204,11 @@ def main():
         step()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st = step()
+    for i in range(args.steps):
+        # the last timed step also records HIP events around every kernel (on
+        # the renderer's stream) for the per-kernel times of the roofline;
+        # their small overhead stays inside the timed region
+        ts = step(timing=(i == args.steps - 1))
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -158,16 +216,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # one extra, untimed step with per-kernel HIP events for the roofline
-    ts = step(timing=True)
     samples_per_step = args.width * args.height * args.spp
     value = world * samples_per_step * args.steps / elapsed / 1e6
 
     if rank == 0:
-        launches = max(ts["iterations"], 1)
-        bytes_total = ts["rays_closest"] * 48 + launches * ts["scene_bytes"]
-        achieved = bytes_total / (ts["ms_extend"] / 1e3) / 1e9 if ts["ms_extend"] > 0 else 0.0
-        traffic = load_traffic(ts)
         out = {
             "metric": METRIC,
             "value": value,
@@ -185,11 +237,7 @@ def main():
                        "scene": "scenes/pa4/cbox/cbox_path_mis.xml", "integrator": "path_mis",
                        "parallelism": f"pass-range sharding x{world}, RCCL film all_reduce" if world > 1
                        else "single GPU", "path_pool": args.pool or 4194304},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_extend (closest-hit traversal)",
-                         "bytes_per_launch": bytes_total / launches,
-                         "avg_launch_ms": ts["ms_extend"] / launches, "launches": launches},
+            "roofline": roofline(ts, samples_per_step),
             "kernel_ms": {"extend": ts["ms_extend"], "shadow": ts["ms_shadow"], "shade": ts["ms_shade"],
                           "splat": ts["ms_splat"], "finish": ts["ms_finish"], "wall": ts["ms_total"]},
             "rays_per_sample": {"closest": ts["rays_closest"] / samples_per_step,

@@ -398,22 +398,23 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQue
                                                              uint32_t G) {
     const SegRange sr = seg_range_k(cnt, G, K);
     const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
+    if (i0 >= n) return;  // entries fill the slice from its start
     TRay r[K];
     bool live[K];
     uint32_t q[K];
+    // lanes past the end load entry i0 again (unconditional loads: no
+    // branch, so all of them are in flight together)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t i = i0 + k * kTraceBlock;
         live[k] = i < n;
-        q[k] = live[k] ? seg_entry(sr, i) : 0u;
-        float4 a = live[k] ? pq.ray_o[q[k]] : make_float4(0, 0, 0, 0);
-        float4 b = live[k] ? pq.ray_d[q[k]] : make_float4(0, 0, 1, 0);
+        q[k] = seg_entry(sr, live[k] ? i : i0);
+        float4 a = pq.ray_o[q[k]], b = pq.ray_d[q[k]];
         r[k].o = ld3(a);
         r[k].d = ld3(b);
         r[k].mint = a.w;
         r[k].maxt = b.w;
     }
-    if (!live[0]) return;  // entries fill the slice from its start
     float t[K], u[K], v[K];
     uint32_t p[K];
     bool f[K];
@@ -428,34 +429,36 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
                                                              float4 *rec, uint32_t G) {
     const SegRange sr = seg_range_k(shcnt, G, K);
     const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
+    if (i0 >= n) return;
     TRay r[K];
     bool live[K], valid[K];
     uint32_t q[K];
+    // unconditional loads (lanes past the end repeat entry i0); payload and
+    // record are fetched before the scan, for occluded rays too, so their
+    // latency hides behind the traversal instead of stalling the wave's end
+    float4 c[K], L[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t i = i0 + k * kTraceBlock;
         valid[k] = live[k] = i < n;
-        q[k] = live[k] ? seg_entry(sr, i) : 0u;
-        float4 a = live[k] ? sq.ray_o[q[k]] : make_float4(0, 0, 0, 0);
-        float4 b = live[k] ? sq.ray_d[q[k]] : make_float4(0, 0, 1, 0);
+        q[k] = seg_entry(sr, live[k] ? i : i0);
+        float4 a = sq.ray_o[q[k]], b = sq.ray_d[q[k]];
+        c[k] = sq.payload[q[k]];
         r[k].o = ld3(a);
         r[k].d = ld3(b);
         r[k].mint = a.w;
         r[k].maxt = b.w;
     }
-    if (!valid[0]) return;
+#pragma unroll
+    for (int k = 0; k < K; ++k) L[k] = rec[__float_as_uint(c[k].w)];
     float t[K], u[K], v[K];
     uint32_t p[K];
     bool f[K];
     scan_rays<K, true>(S, r, live, t, p, u, v, f);
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        if (valid[k] && !f[k]) {
-            float4 c = sq.payload[q[k]];
-            uint32_t w = __float_as_uint(c.w);
-            float4 L = rec[w];
-            rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
-        }
+        if (valid[k] && !f[k])
+            rec[__float_as_uint(c[k].w)] = make_float4(L[k].x + c[k].x, L[k].y + c[k].y, L[k].z + c[k].z, L[k].w);
 }
 
 // ------------------------------------------------------------------ shading helpers
@@ -588,11 +591,194 @@ ND void store_path(const PathQueue &Q, uint32_t i, const PathState &ps) {
     Q.work[i] = ps.work;
 }
 
+// ------------------------------------------------------------------ medium
+// HomogeneousMedium (medium.cpp:22-94): box = origin -/+ |size|, sigma_t =
+// sigma_a + sigma_s, albedo = sigma_s / sigma_t, isotropic phase function
+// (phasefunction.cpp:13-16).
+// BoundingBox3f::rayIntersect(ray, nearT, farT) (bbox.h:366-393) for the ray
+// (o, d) with dRcp = 1/d; a NaN direction leaves the slab test false.
+ND bool mbox_range(const DevScene &S, V3 o, V3 d, float &nearT, float &farT) {
+    nearT = -INF_F;
+    farT = INF_F;
+    const float oc[3] = {o.x, o.y, o.z}, dc[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float origin = oc[i], mn = S.mbox_min[i], mx = S.mbox_max[i];
+        if (dc[i] == 0.0f) {
+            if (origin < mn || origin > mx) return false;
+        } else {
+            const float r = 1.0f / dc[i];
+            float t1 = (mn - origin) * r, t2 = (mx - origin) * r;
+            if (t1 > t2) {
+                float t = t1;
+                t1 = t2;
+                t2 = t;
+            }
+            nearT = smax(t1, nearT);
+            farT = smin(t2, farT);
+            if (!(nearT <= farT)) return false;
+        }
+    }
+    return true;
+}
+ND bool mbox_contains(const DevScene &S, V3 p) {  // bbox.h:115-123 (non-strict)
+    return p.x >= S.mbox_min[0] && p.y >= S.mbox_min[1] && p.z >= S.mbox_min[2] && p.x <= S.mbox_max[0] &&
+           p.y <= S.mbox_max[1] && p.z <= S.mbox_max[2];
+}
+// HomogeneousMedium::Tr(src, dst): transmittance over the part of [src, dst]
+// inside the box.  Tr(p, p) has a NaN direction and is 1, as in the reference.
+ND V3 medium_tr(const DevScene &S, V3 src, V3 dst) {
+    if (!S.has_medium) return V3{1, 1, 1};
+    const V3 d = normalize(dst - src);
+    float nearT, farT;
+    if (!mbox_range(S, src, d, nearT, farT)) return V3{1, 1, 1};
+    const V3 sp = mbox_contains(S, src) ? src : src + normalize(d) * nearT;
+    const V3 ep = mbox_contains(S, dst) ? dst : src + normalize(d) * farT;
+    const float n = norm(ep - sp);
+    return V3{expf(-S.sigma_t[0] * n), expf(-S.sigma_t[1] * n), expf(-S.sigma_t[2] * n)};
+}
+// HomogeneousMedium::sample: free-flight distance from the box entry point;
+// true (and p) when the ray scatters before tmax.  No random number is drawn
+// for a ray that misses the box.
+ND bool medium_sample(const DevScene &S, V3 o, V3 d, Pcg &rng, float tmax, V3 &p) {
+    if (!S.has_medium) return false;
+    float nearT, farT;
+    if (!mbox_range(S, o, d, nearT, farT)) return false;
+    const V3 sp = mbox_contains(S, o) ? o : o + normalize(d) * nearT;
+    const float st = smax(smax(S.sigma_t[0], S.sigma_t[1]), S.sigma_t[2]);
+    const float distance = norm(sp - o) + (-1.0f * logf(1 - next1D(rng)) / st);  // invTr
+    if (distance >= tmax) return false;
+    p = o + d * distance;  // Ray3f::operator()
+    return true;
+}
+
+// Next-event estimation from x (AreaEmitter::sample, arealight.cpp:52-68):
+// one emitter chosen uniformly (scene.h:68-74), Li already scaled by N.
+struct NeeSample {
+    V3 p, wi, Li;
+    float pdf_em, dist;
+    int emitter;
+};
+ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
+    NeeSample r;
+    const float ul = next1D(rng);
+    const uint32_t N = S.num_emitters;
+    uint32_t li = (uint32_t)floorf((float)N * ul);
+    if (li > N - 1) li = N - 1;
+    const DevEmitter &E = S.emitters[li];
+    const V2 s2 = next2D(rng);
+    V3 ln;
+    sample_surface(S, S.shapes[E.shape], s2, r.p, ln);
+    const V3 dv = r.p - x;
+    r.wi = normalize(dv);
+    r.pdf_em = emitter_pdf(S, E, ln, r.wi);
+    const float att = dot(ln, -r.wi) / dot(dv, dv);
+    V3 Li = r.pdf_em > 0.0f ? (emitter_eval(E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
+    r.Li = Li * (float)N;
+    r.dist = norm(dv);
+    r.emitter = (int)li;
+    return r;
+}
+
+// One iteration of VolumetricIntegrator::Li (volumetric.cpp:18-156) for the
+// current segment (ps.o, ps.d) and its closest hit h (prim ~0: none, t = inf).
+// Free flight first: a scattering event does phase-function NEE with
+// transmittance, Russian roulette at 0.8 and a uniform-sphere bounce; else
+// the surface vertex does path_mis-style emission and NEE, both weighted by
+// transmittance.  ps.prev carries the pdf for w_mats at the next emitter hit
+// (1/4pi after a scattering event, -1 after a discrete lobe).
+ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
+    so.emit = false;
+    const uint32_t prim = __float_as_uint(h.y);
+    const bool inter = prim != 0xFFFFFFFFu;
+    SurfHit hs;
+    float tmax = INF_F;
+    if (inter) {
+        hs = surface(S, prim, h.x, h.z, h.w, ps.o, ps.d);
+        tmax = norm(hs.p - ps.o);
+    }
+    V3 mp;
+    if (medium_sample(S, ps.o, ps.d, ps.rng, tmax, mp)) {
+        const V3 wo = sq_uniform_sphere(next2D(ps.rng));
+        const float pdf_mat = kInvFourPi;
+        NeeSample ne = nee_sample(S, mp, ps.rng);
+        ps.beta = ps.beta * V3{S.albedo[0], S.albedo[1], S.albedo[2]};
+        const V3 tr = medium_tr(S, mp, ne.p);
+        so.contrib = ((ps.beta * tr) * ne.Li) * pdf_mat;
+        so.emit = !is_zero(so.contrib);
+        so.o = mp;
+        so.d = ne.wi;
+        so.maxt = ne.dist - kEps;
+        so.work = ps.work;
+        const float q = smin(ps.beta.x, 0.80f);
+        if (next1D(ps.rng) > q) return false;
+        ps.beta = ps.beta / q;
+        ps.o = mp;
+        ps.d = normalize(wo);
+        ps.mint = kEps;
+        ps.maxt = INF_F;
+        ps.prev = pdf_mat;
+        return true;
+    }
+    if (!inter) return false;  // escaped (volumetric.cpp: break)
+    const DevShape &sh = S.shapes[hs.shape];
+    const DevBsdf &B = S.bsdfs[sh.bsdf];
+    if (sh.emitter >= 0) {
+        const DevEmitter &E = S.emitters[sh.emitter];
+        const V3 wi = normalize(hs.p - ps.o);
+        const V3 Le = emitter_eval(E, hs.sh.n, wi);
+        float w = 1.0f;
+        if (ps.prev >= 0.0f) {
+            const float pe = emitter_pdf(S, E, hs.sh.n, wi);
+            w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
+        }
+        const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
+        float4 L = rec[ps.work];
+        rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, L.w);
+    }
+    {
+        NeeSample ne = nee_sample(S, hs.p, ps.rng);
+        BRec br;
+        br.wi = to_local(hs.sh, -ps.d);
+        br.wo = to_local(hs.sh, ne.wi);
+        br.measure = kMeasureSolidAngle;
+        const float theta = smax(0.0f, br.wo.z);
+        const V3 f = bsdf_eval(B, br);
+        const float pdf_mat = bsdf_pdf(B, br);
+        const float w_ems = (pdf_mat + ne.pdf_em) > 0.0f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
+        const V3 tr = medium_tr(S, hs.p, ne.p);
+        so.contrib = ((((ps.beta * w_ems) * f) * theta) * ne.Li) * tr;
+        so.emit = !is_zero(so.contrib);
+        so.o = hs.p;
+        so.d = ne.wi;
+        so.maxt = ne.dist - kEps;
+        so.work = ps.work;
+    }
+    const float q = smin(ps.beta.x, 0.80f);
+    if (next1D(ps.rng) > q) return false;
+    ps.beta = ps.beta / q;
+    BRec br;
+    br.wi = to_local(hs.sh, -ps.d);
+    br.wo = V3{0, 0, 1};
+    br.measure = kMeasureUnknown;
+    const V3 w = bsdf_sample(B, br, next2D(ps.rng));
+    if (is_zero(w)) return false;  // deviation D1
+    ps.beta = ps.beta * w;
+    const float pm = bsdf_pdf(B, br);
+    ps.prev = br.measure == kMeasureDiscrete ? -1.0f : pm;
+    ps.o = hs.p;
+    ps.d = to_world(hs.sh, br.wo);
+    ps.mint = kEps;
+    ps.maxt = INF_F;
+    return true;
+}
+
 // One vertex of PathMisIntegrator::Li (path_mis.cpp:32-97) or
 // PathMatsIntegrator::Li (path_mats.cpp:26-57) given the closest hit of the
 // current ray.  Returns true if the path continues (ps holds the new ray).
 template <int INTEG>
 ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
+    if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol(S, ps, h, rec, so);
     so.emit = false;
     uint32_t prim = __float_as_uint(h.y);
     if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
@@ -1097,25 +1283,28 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
                    : trace_dispatch<false>(S, rays, n, hits, stack, st);
 }
 
+template <int INTEG>
+static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
+                           const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
+                           uint32_t lds, hipStream_t st) {
+    dim3 g(wd.G), b(kShadeBlock);
+    if (trace)
+        hipLaunchKernelGGL((k_shade<INTEG, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+    else
+        hipLaunchKernelGGL((k_shade<INTEG, false>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+}
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                         hipStream_t st) {
-    dim3 g(wd.G), b(kShadeBlock);
     const uint32_t lds = S.blob_bytes <= kShadeLdsMax ? S.blob_bytes : 0u;
-    if (trace) {
-        if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS, true>), g, b, lds, st, S, in, out, sq, seg, in_sel,
-                               wd, rec, C, lds);
-        else
-            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS, true>), g, b, lds, st, S, in, out, sq, seg, in_sel,
-                               wd, rec, C, lds);
-    } else {
-        if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MATS, false>), g, b, lds, st, S, in, out, sq, seg, in_sel,
-                               wd, rec, C, lds);
-        else
-            hipLaunchKernelGGL((k_shade<NORI_INTEGRATOR_PATH_MIS, false>), g, b, lds, st, S, in, out, sq, seg, in_sel,
-                               wd, rec, C, lds);
+    switch (S.integrator) {
+    case NORI_INTEGRATOR_PATH_MATS:
+        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, st);
+        break;
+    case NORI_INTEGRATOR_VOLUMETRIC:
+        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, st);
+        break;
+    default: shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, st); break;
     }
     return hipGetLastError();
 }
@@ -1177,6 +1366,8 @@ hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st) {
     if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
         finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
+    else if (S.integrator == NORI_INTEGRATOR_VOLUMETRIC)
+        finish_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
     else
         finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
     return hipGetLastError();

@@ -288,8 +288,13 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         for (int k = 0; k < 3; ++k) emitters[i].radiance[k] = e.radiance[k];
     }
     if (d.num_emitters == 0) throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
-    if (d.integrator != NORI_INTEGRATOR_PATH_MIS && d.integrator != NORI_INTEGRATOR_PATH_MATS)
-        throw NoriException(NORI_ERR_UNSUPPORTED, "integrator not yet on the GPU path");
+    if (d.integrator != NORI_INTEGRATOR_PATH_MIS && d.integrator != NORI_INTEGRATOR_PATH_MATS &&
+        d.integrator != NORI_INTEGRATOR_VOLUMETRIC)
+        throw NoriException(NORI_ERR_UNSUPPORTED, "unknown integrator");
+    // the reference leaves Scene::m_medium uninitialised without a <medium>
+    // (scene.h:141): rejected here, as in the oracle
+    if (d.integrator == NORI_INTEGRATOR_VOLUMETRIC && !d.medium.present)
+        throw NoriException(NORI_ERR_INVALID, "the volumetric integrator needs a <medium>");
 
     DeviceBvh bvh;
     build_device_bvh(d, rmin, rmax, bvh);
@@ -423,6 +428,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     if (S.border > 4) throw NoriException(NORI_ERR_UNSUPPORTED, "filter radius above 4.5 pixels");
     S.integrator = d.integrator;
     S.has_medium = d.medium.present;
+    if (S.has_medium) {  // medium.cpp:10-20
+        const nori_medium_desc &m = d.medium;
+        for (int k = 0; k < 3; ++k) {
+            S.mbox_min[k] = m.box_min[k];
+            S.mbox_max[k] = m.box_max[k];
+            S.sigma_t[k] = m.sigma_a[k] + m.sigma_s[k];
+            S.albedo[k] = m.sigma_s[k] / S.sigma_t[k];
+        }
+    }
 }
 
 void ensure_pool(nori_gpu_ctx &c, uint32_t pool) {
