@@ -20,6 +20,7 @@
  *   nori_gpu_progress     <- RenderThread::getProgress    src/render.cpp:73-78
  *   nori_film_develop     <- ImageBlock::toBitmap         src/block.cpp:76-82
  *   nori_write_exr        <- Bitmap::save                 src/bitmap.cpp:82-107
+ *   nori_read_exr         <- Bitmap::Bitmap(filename)     src/bitmap.cpp:23-80
  *
  * Rules of the ABI: plain C types only, no exceptions cross it, every call
  * returns an int status (NORI_OK = 0, negative = error) and the message of
@@ -170,6 +171,10 @@ int nori_filter_table(const nori_scene_desc *scene, float table[NORI_FILTER_RESO
 int nori_film_develop(const nori_scene_desc *scene, const float *rgbw, float *rgb);
 /* Write an RGB float image as an uncompressed scanline OpenEXR file. */
 int nori_write_exr(const char *path, const float *rgb, int width, int height);
+/* Read the R, G, B planes of a scanline OpenEXR file (NONE/ZIPS/ZIP, HALF or
+ * FLOAT) <- Bitmap::Bitmap (bitmap.cpp:23-80).  Call with rgb = NULL to get
+ * the size, then with a buffer of 3*width*height floats (row-major). */
+int nori_read_exr(const char *path, int *width, int *height, float *rgb);
 
 /* ---- GPU context ----------------------------------------------------------- */
 typedef struct nori_gpu_ctx nori_gpu_ctx;

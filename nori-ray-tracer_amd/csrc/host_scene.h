@@ -37,6 +37,7 @@ struct HostScene {
     std::vector<nori_shape_desc> shapes;
     std::vector<nori_bsdf_desc> bsdfs;
     std::vector<nori_emitter_desc> emitters;
+    std::vector<std::vector<float>> env_images;  // envmap texels, owned here (emitters[i].env_rgb)
     nori_scene_desc desc{};
     float root_min[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float root_max[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
@@ -50,6 +51,8 @@ struct HostScene {
     void finalize();
 };
 HostScene *load_scene_xml(const std::string &path, int width, int height, int spp);
+// R, G, B planes of an OpenEXR file, rows = image height (image_io.cpp); throws NoriException.
+int load_exr(const std::string &path, int &width, int &height, std::vector<float> &rgb);
 
 // ---- BVH in device layout -------------------------------------------------
 // Inner node = 4 x float4 (64 B, one cache line):

@@ -455,6 +455,24 @@ struct AreaEmitter : Emitter {  // arealight.cpp:25-28
     }
 };
 NORI_REGISTER_CLASS(AreaEmitter, "area")
+struct EnvMapEmitter : Emitter {  // envmap.cpp:13-58
+    explicit EnvMapEmitter(const PropertyList &p) {
+        d.type = NORI_EMITTER_ENVMAP;
+        d.shape = -1;
+        d.weight = p.getFloat("weight", 1.0f);
+        std::string fn = resolve_path(p.getString("filename", "textures/envmaptext.exr"));
+        Vec3f ls = p.getVector3("luminanceScale", Vec3f{0.3f, 0.6f, 0.1f});
+        d.lum_scale[0] = ls.x;
+        d.lum_scale[1] = ls.y;
+        d.lum_scale[2] = ls.z;
+        int w = 0, h = 0;
+        load_exr(fn, w, h, rgb);
+        d.env_rows = h;  // Bitmap rows = scanlines (the envmap's "m_width")
+        d.env_cols = w;
+        if (h < 2 || w < 2) throw NoriException(NORI_ERR_INVALID, "EnvMap: the image needs at least 2x2 texels");
+    }
+};
+NORI_REGISTER_CLASS(EnvMapEmitter, "envmap")
 
 // ---- shapes
 struct Shape : NoriObject {
@@ -992,6 +1010,10 @@ HostScene *load_scene_xml(const std::string &path, int width, int height, int sp
     }
     for (Emitter *e : sc->emitters) {
         nori_emitter_desc ed = e->d;
+        if (ed.type == NORI_EMITTER_ENVMAP) {
+            hs->env_images.push_back(e->rgb);
+            ed.env_rgb = hs->env_images.back().data();
+        }
         for (size_t si = 0; si < sc->shapes.size(); ++si)
             if (sc->shapes[si]->emitter == e) {
                 ed.shape = (int32_t)si;

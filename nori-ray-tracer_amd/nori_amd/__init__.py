@@ -127,6 +127,15 @@ def write_exr(path, rgb):
     check(lib().nori_write_exr(os.fsencode(path), _fptr(rgb), rgb.shape[1], rgb.shape[0]))
 
 
+def read_exr(path):
+    """R, G, B planes of an OpenEXR file as a (height, width, 3) float32 array (nori_read_exr)."""
+    w, h = C.c_int(), C.c_int()
+    check(lib().nori_read_exr(os.fsencode(path), C.byref(w), C.byref(h), None))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    check(lib().nori_read_exr(os.fsencode(path), C.byref(w), C.byref(h), _fptr(out)))
+    return out
+
+
 class GpuRenderer:
     """HIP context holding one scene on one device (nori_gpu_create)."""
 
