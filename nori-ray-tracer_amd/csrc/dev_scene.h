@@ -30,10 +30,16 @@ struct DevShape {
     float pad2[3];
 };
 
+// 64 B.  Area: radiance.  Envmap (envmap.cpp): R x C texels (R = Bitmap rows,
+// the reference's m_width), tables at float offsets into DevScene::env:
+// rgb R*C*3, pdf R*C, cdf R*(C+1), marginal pdf R, marginal cdf R+1.
 struct DevEmitter {
     int32_t type, shape;
     float radiance[3];
-    float pad[3];
+    float weight;
+    int32_t R, C;
+    uint32_t rgb_off, pdf_off, cdf_off, pmarg_off, cmarg_off;
+    uint32_t pad[3];
 };
 
 struct DevScene {
@@ -47,6 +53,7 @@ struct DevScene {
     const DevBsdf *bsdfs;
     const DevEmitter *emitters;
     const float *cdf;
+    const float *env;  // envmap tables (DevEmitter offsets), global memory
     uint32_t num_emitters;
     uint32_t num_nodes;
     uint32_t num_prims;

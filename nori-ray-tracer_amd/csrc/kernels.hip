@@ -492,11 +492,78 @@ ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, 
     return h;
 }
 
-// AreaEmitter (arealight.cpp:39-76)
+// EnvironmentMap (envmap.cpp), restated as the oracle's env_* functions.
+constexpr float kEnvTFar = 100000.0f;  // envmap.cpp:9
+// sphericalCoordinates (common.cpp:264-272) + mapIntersect (envmap.cpp:61-75)
+ND V2 env_map(const DevEmitter &e, V3 vec) {
+    float theta = acosf(vec.z), phi = atan2f(vec.y, vec.x);
+    if (phi < 0) phi = (float)((double)phi + 2 * M_PI);
+    V2 uv;
+    uv.x = theta * (float)(e.R - 1) * kInvPi;
+    uv.y = (float)((double)phi * 0.5 * (double)(e.C - 1) * (double)kInvPi);
+    if (isnan(uv.x) || isnan(uv.y)) uv = V2{0, 0};
+    return uv;
+}
+ND int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+ND V3 env_texel(const DevScene &S, const DevEmitter &e, int i, int j) {
+    const float *c = S.env + e.rgb_off + 3 * ((size_t)i * e.C + j);
+    return V3{c[0], c[1], c[2]};
+}
+// EnvironmentMap::eval (envmap.cpp:124-156): bilinear, wrapping at the edges
+ND V3 env_eval(const DevScene &S, const DevEmitter &e, V3 wi) {
+    const V2 uv = env_map(e, normalize(wi));
+    const int u = clampi((int)uv.x, 0, e.R - 1), v = clampi((int)uv.y, 0, e.C - 1);
+    const int us = (u + 1) % e.R, vs = (v + 1) % e.C;
+    const V3 BL = env_texel(S, e, u, v), UL = env_texel(S, e, u, vs), BR = env_texel(S, e, us, v),
+             UR = env_texel(S, e, us, vs);
+    const int dusu = us - u, dvsv = vs - v;
+    const float dusum = (float)us - uv.x, dumu = uv.x - (float)u, dvmv = uv.y - (float)v, dvsvm = (float)vs - uv.y;
+    const V3 acc = ((((BL * dusum) * dvsvm) + ((BR * dumu) * dvsvm)) + ((UL * dusum) * dvmv)) + ((UR * dumu) * dvmv);
+    const float inv = (float)(1.0 / (double)(dusu * dvsv));
+    const V3 r = V3{inv * acc.x, inv * acc.y, inv * acc.z};
+    return V3{e.weight * r.x, e.weight * r.y, e.weight * r.z};
+}
+// EnvironmentMap::pdf (envmap.cpp:184-192)
+ND float env_pdf(const DevScene &S, const DevEmitter &e, V3 wi) {
+    const V2 uv = env_map(e, normalize(wi));
+    const int i = clampi((int)uv.x, 0, e.R - 1), j = clampi((int)uv.y, 0, e.C - 1);
+    return S.env[e.pmarg_off + i] * S.env[e.pdf_off + (size_t)i * e.C + j];
+}
+// sample1D (envmap.cpp:112-122); an all-zero row takes its last interval
+ND void env_sample1D(const float *pf, const float *P, int cols, float s, float &x, float &prob) {
+    int i;
+    for (i = 0; i < cols; i++)
+        if (P[i] <= s && s < P[i + 1]) break;
+    if (i >= cols) i = cols - 1;
+    const float t = (P[i + 1] - s) / (P[i + 1] - P[i]);
+    x = (1 - t) * (float)i + t * (float)(i + 1);
+    prob = pf[i];
+}
+// EnvironmentMap::sample (envmap.cpp:158-181); deviation D4: the Jacobian
+// uses the sampled direction (the reference reads lRec.wi uninitialised).
+ND V3 env_sample(const DevScene &S, const DevEmitter &e, V2 smp, V3 &wi) {
+    float u, v, u_pdf, v_pdf;
+    env_sample1D(S.env + e.pmarg_off, S.env + e.cmarg_off, e.R, smp.x, u, u_pdf);
+    const int row = (int)u;
+    env_sample1D(S.env + e.pdf_off + (size_t)row * e.C, S.env + e.cdf_off + (size_t)row * (e.C + 1), e.C, smp.y, v,
+                 v_pdf);
+    const float theta = (float)((double)u * M_PI / (double)(e.R - 1));  // invMapIntersect
+    const float phi = (float)((double)(v * 2.0f) * M_PI / (double)(e.C - 1));
+    wi = normalize(V3{sinf(theta) * cosf(phi), sinf(theta) * sinf(phi), cosf(theta)});
+    const float st2 = 1.0f - wi.z * wi.z, st = st2 <= 0.0f ? 0.0f : sqrtf(st2);  // Frame::sinTheta
+    const float jac = (float)((double)((e.C - 1) * (e.R - 1)) / (2 * (M_PI * M_PI) * (double)st));
+    v_pdf = env_pdf(S, e, wi) * jac;
+    const V3 c = env_eval(S, e, wi);
+    return V3{c.x / v_pdf, c.y / v_pdf, c.z / v_pdf};
+}
+
+// AreaEmitter (arealight.cpp:39-76) or EnvironmentMap
 ND float emitter_pdf(const DevScene &S, const DevEmitter &e, V3 n, V3 wi) {
+    if (e.type == NORI_EMITTER_ENVMAP) return env_pdf(S, e, wi);
     return dot(n, -wi) > 0.0f ? S.shapes[e.shape].area_norm : 0.0f;
 }
-ND V3 emitter_eval(const DevEmitter &e, V3 n, V3 wi) {
+ND V3 emitter_eval(const DevScene &S, const DevEmitter &e, V3 n, V3 wi) {
+    if (e.type == NORI_EMITTER_ENVMAP) return env_eval(S, e, wi);
     return dot(n, -wi) > 0.0f ? V3{e.radiance[0], e.radiance[1], e.radiance[2]} : V3{0, 0, 0};
 }
 // Shape::sampleSurface: Mesh (mesh.cpp:40-58, DiscretePDF::sampleReuse
@@ -656,8 +723,7 @@ ND bool medium_sample(const DevScene &S, V3 o, V3 d, Pcg &rng, float tmax, V3 &p
 // one emitter chosen uniformly (scene.h:68-74), Li already scaled by N.
 struct NeeSample {
     V3 p, wi, Li;
-    float pdf_em, dist;
-    int emitter;
+    float pdf_em, maxt;  // maxt: of the shadow ray from x
 };
 ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
     NeeSample r;
@@ -667,16 +733,23 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
     if (li > N - 1) li = N - 1;
     const DevEmitter &E = S.emitters[li];
     const V2 s2 = next2D(rng);
+    if (E.type == NORI_EMITTER_ENVMAP) {
+        const V3 Li = env_sample(S, E, s2, r.wi);
+        r.Li = Li * (float)N;
+        r.pdf_em = env_pdf(S, E, r.wi);
+        r.maxt = kEnvTFar;               // shadow ray (ref, wi, Epsilon, T_FAR)
+        r.p = x + r.wi * kEnvTFar;       // D4: lRec.p is never set by the reference
+        return r;
+    }
     V3 ln;
     sample_surface(S, S.shapes[E.shape], s2, r.p, ln);
     const V3 dv = r.p - x;
     r.wi = normalize(dv);
     r.pdf_em = emitter_pdf(S, E, ln, r.wi);
     const float att = dot(ln, -r.wi) / dot(dv, dv);
-    V3 Li = r.pdf_em > 0.0f ? (emitter_eval(E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
+    V3 Li = r.pdf_em > 0.0f ? (emitter_eval(S, E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
     r.Li = Li * (float)N;
-    r.dist = norm(dv);
-    r.emitter = (int)li;
+    r.maxt = norm(dv) - kEps;
     return r;
 }
 
@@ -708,7 +781,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
         so.emit = !is_zero(so.contrib);
         so.o = mp;
         so.d = ne.wi;
-        so.maxt = ne.dist - kEps;
+        so.maxt = ne.maxt;
         so.work = ps.work;
         const float q = smin(ps.beta.x, 0.80f);
         if (next1D(ps.rng) > q) return false;
@@ -726,7 +799,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     if (sh.emitter >= 0) {
         const DevEmitter &E = S.emitters[sh.emitter];
         const V3 wi = normalize(hs.p - ps.o);
-        const V3 Le = emitter_eval(E, hs.sh.n, wi);
+        const V3 Le = emitter_eval(S, E, hs.sh.n, wi);
         float w = 1.0f;
         if (ps.prev >= 0.0f) {
             const float pe = emitter_pdf(S, E, hs.sh.n, wi);
@@ -751,7 +824,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
         so.emit = !is_zero(so.contrib);
         so.o = hs.p;
         so.d = ne.wi;
-        so.maxt = ne.dist - kEps;
+        so.maxt = ne.maxt;
         so.work = ps.work;
     }
     const float q = smin(ps.beta.x, 0.80f);
@@ -788,7 +861,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     if (sh.emitter >= 0) {  // emission (path_mis.cpp:35-39, path_mats.cpp:31-35)
         const DevEmitter &E = S.emitters[sh.emitter];
         V3 wi = normalize(hs.p - ps.o);
-        V3 Le = emitter_eval(E, hs.sh.n, wi);
+        V3 Le = emitter_eval(S, E, hs.sh.n, wi);
         V3 Ladd;
         if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
             float w = 1.0f;  // w_mats (path_mis.cpp:87-97)
@@ -804,33 +877,20 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, L.w);
     }
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
-        float ul = next1D(ps.rng);
-        uint32_t N = S.num_emitters;
-        uint32_t li = (uint32_t)floorf((float)N * ul);
-        if (li > N - 1) li = N - 1;
-        const DevEmitter &E = S.emitters[li];
-        V2 s2 = next2D(ps.rng);
-        V3 lp, ln;
-        sample_surface(S, S.shapes[E.shape], s2, lp, ln);
-        V3 dv = lp - hs.p;
-        V3 wi = normalize(dv);
-        float pdf_em = emitter_pdf(S, E, ln, wi);
-        float att = dot(ln, -wi) / dot(dv, dv);
-        V3 Li = pdf_em > 0.0f ? (emitter_eval(E, ln, wi) * att) / pdf_em : V3{0, 0, 0};
-        Li = Li * (float)N;
+        const NeeSample ne = nee_sample(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
-        br.wo = to_local(hs.sh, wi);
+        br.wo = to_local(hs.sh, ne.wi);
         br.measure = kMeasureSolidAngle;
         float theta = smax(0.0f, br.wo.z);
         V3 f = bsdf_eval(B, br);
         float pdf_mat = bsdf_pdf(B, br);
-        float w_ems = (pdf_mat + pdf_em) > 0.0f ? pdf_em / (pdf_mat + pdf_em) : pdf_em;
-        so.contrib = (((ps.beta * w_ems) * f) * theta) * Li;
+        float w_ems = (pdf_mat + ne.pdf_em) > 0.0f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
+        so.contrib = (((ps.beta * w_ems) * f) * theta) * ne.Li;
         so.emit = !is_zero(so.contrib);  // a zero contribution adds nothing (NaN still goes)
         so.o = hs.p;
-        so.d = wi;
-        so.maxt = norm(dv) - kEps;
+        so.d = ne.wi;
+        so.maxt = ne.maxt;
         so.work = ps.work;
     }
     // Russian roulette on the red channel (path_mis.cpp:64-69)

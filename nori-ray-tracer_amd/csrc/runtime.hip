@@ -98,6 +98,54 @@ static void filter_table(const nori_camera_desc &c, float *t) {
     t[NORI_FILTER_RESOLUTION] = 0.0f;
 }
 
+// EnvironmentMap tables (envmap.cpp:13-58, 91-109), appended to `env`.
+// precompute1D literally: res is the LAST value of `i + f(row, i)`, and the CDF
+// accumulates pf(i - 1), a column-major linear index into the whole pf matrix
+// (rows not yet computed read as 0, as from a fresh allocation).
+static float env_precompute1D(int row, const float *f, int cols, float *pf, float *Pf, int pf_rows) {
+    float res = 0;
+    int i;
+    for (i = 0; i < cols; i++) res = (float)i + f[(size_t)row * cols + i];
+    if (res == 0) return res;
+    for (int j = 0; j < cols; j++) pf[(size_t)row * cols + j] = f[(size_t)row * cols + j] / res;
+    Pf[(size_t)row * (cols + 1)] = 0;
+    for (i = 1; i < cols; i++) {
+        const int k = i - 1;
+        Pf[(size_t)row * (cols + 1) + i] =
+            Pf[(size_t)row * (cols + 1) + i - 1] + pf[(size_t)(k % pf_rows) * cols + (k / pf_rows)];
+    }
+    Pf[(size_t)row * (cols + 1) + i] = 1;
+    return res;
+}
+static void build_envmap(const nori_emitter_desc &e, DevEmitter &o, std::vector<float> &env) {
+    const int R = e.env_rows, C = e.env_cols;
+    if (R < 2 || C < 2 || !e.env_rgb) throw NoriException(NORI_ERR_INVALID, "EnvMap: the image needs at least 2x2 texels");
+    o.weight = e.weight;
+    o.R = R;
+    o.C = C;
+    auto grab = [&](size_t n) {
+        const size_t off = env.size();
+        env.resize(off + n, 0.0f);
+        return (uint32_t)off;
+    };
+    o.rgb_off = grab(3 * (size_t)R * C);
+    std::memcpy(&env[o.rgb_off], e.env_rgb, 12 * (size_t)R * C);
+    o.pdf_off = grab((size_t)R * C);
+    o.cdf_off = grab((size_t)R * (C + 1));
+    o.pmarg_off = grab((size_t)R);
+    o.cmarg_off = grab((size_t)R + 1);
+    if (env.size() >= (1ull << 32)) throw NoriException(NORI_ERR_UNSUPPORTED, "EnvMap: tables above 4G floats");
+    std::vector<float> lum((size_t)R * C), sum((size_t)R);
+    for (int i = 0; i < R; i++)
+        for (int j = 0; j < C; j++) {
+            const float *c = e.env_rgb + 3 * ((size_t)i * C + j);
+            lum[(size_t)i * C + j] =
+                std::sqrt((e.lum_scale[0] * c[0] + e.lum_scale[1] * c[1]) + e.lum_scale[2] * c[2]) + kEps / 10000000;
+        }
+    for (int i = 0; i < R; ++i) sum[i] = env_precompute1D(i, lum.data(), C, &env[o.pdf_off], &env[o.cdf_off], R);
+    env_precompute1D(0, sum.data(), R, &env[o.pmarg_off], &env[o.cmarg_off], 1);
+}
+
 // BlockGenerator spiral (block.cpp:140-188)
 static std::vector<uint32_t> spiral_blocks(int W, int H) {
     int nx = (int)std::ceil(W / (float)NORI_BLOCK_SIZE), ny = (int)std::ceil(H / (float)NORI_BLOCK_SIZE);
@@ -138,7 +186,7 @@ struct nori_gpu_ctx {
     hipEvent_t fork = nullptr, join = nullptr;
     DevScene S{};
     nori_camera_desc cam{};
-    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, blob;
+    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob;
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
     uint32_t bvh_depth = 0, bvh_nodes = 0, num_prims = 0;
     size_t scene_bytes = 0;
@@ -278,14 +326,17 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         if (b.type < NORI_BSDF_DIFFUSE || b.type > NORI_BSDF_DISNEY) throw NoriException(NORI_ERR_INVALID, "unknown bsdf type");
     }
     std::vector<DevEmitter> emitters(d.num_emitters);
+    std::vector<float> env;  // envmap tables of every envmap emitter
     for (uint32_t i = 0; i < d.num_emitters; ++i) {
         const nori_emitter_desc &e = d.emitters[i];
-        if (e.type != NORI_EMITTER_AREA) throw NoriException(NORI_ERR_UNSUPPORTED, "only area emitters are on the GPU path this round");
+        if (e.type != NORI_EMITTER_AREA && e.type != NORI_EMITTER_ENVMAP)
+            throw NoriException(NORI_ERR_UNSUPPORTED, "unknown emitter type");
         if (e.shape < 0 || (uint32_t)e.shape >= d.num_shapes) throw NoriException(NORI_ERR_INVALID, "emitter without a shape");
         std::memset(&emitters[i], 0, sizeof(DevEmitter));
         emitters[i].type = e.type;
         emitters[i].shape = e.shape;
         for (int k = 0; k < 3; ++k) emitters[i].radiance[k] = e.radiance[k];
+        if (e.type == NORI_EMITTER_ENVMAP) build_envmap(e, emitters[i], env);
     }
     if (d.num_emitters == 0) throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
     if (d.integrator != NORI_INTEGRATOR_PATH_MIS && d.integrator != NORI_INTEGRATOR_PATH_MATS &&
@@ -358,6 +409,8 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     c.bsdfs.upload(bsdfs);
     c.emitters.upload(emitters);
     c.cdf.upload(cdf);
+    if (env.empty()) env.assign(4, 0.0f);
+    c.env.upload(env);
     c.scene_bytes = c.nodes.bytes + c.prims.bytes;
     // small-scene blob (staged into LDS by the tail finisher)
     std::vector<char> blob;
@@ -393,6 +446,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.bsdfs = c.bsdfs.as<DevBsdf>();
     S.emitters = c.emitters.as<DevEmitter>();
     S.cdf = c.cdf.as<float>();
+    S.env = c.env.as<float>();
     S.num_emitters = d.num_emitters;
     S.num_nodes = bvh.num_nodes;
     S.num_prims = (uint32_t)(prim_list.size() / 12);

@@ -500,6 +500,12 @@ typedef struct {
 typedef struct {
     int type, shape;
     V3 radiance;
+    /* envmap (envmap.cpp:13-58); R = Bitmap rows (the reference's m_width), C = cols (m_height) */
+    int R, C;
+    float weight;
+    const float *rgb;            /* R*C*3, row-major */
+    float *pdf, *cdf;            /* R x C, R x (C+1), row-major */
+    float *pmarg, *cmarg;        /* R, R+1 */
 } Emitter;
 
 typedef struct { uint32_t flag_size; uint32_t start_right; BBox bbox; } Node; /* bvh.h:127-164 */
@@ -850,15 +856,129 @@ static inline float shape_pdf_surface(const Shape *sh) {
     }
     return sh->normalization;
 }
+/* ---- environment map (envmap.cpp) ------------------------------------------ */
+#define ENV_T_FAR 100000.0f  /* envmap.cpp:9 */
+/* precompute1D (envmap.cpp:91-109), literally: res is the LAST value of
+ * `i + f(row, i)`, and the CDF accumulates pf(i - 1), a linear (column-major,
+ * Eigen) index into the whole pf matrix -- rows not yet computed read as 0
+ * (a fresh allocation).  pf_rows = rows of pf, pf_row_major = storage here. */
+static float env_precompute1D(int row, const float *f, int cols, float *pf, float *Pf, int pf_rows) {
+    float res = 0;
+    int i;
+    for (i = 0; i < cols; i++) res = (float)i + f[(size_t)row * cols + i];
+    if (res == 0) return res;
+    for (int j = 0; j < cols; j++) pf[(size_t)row * cols + j] = f[(size_t)row * cols + j] / res;
+    Pf[(size_t)row * (cols + 1) + 0] = 0;
+    for (i = 1; i < cols; i++) {
+        int k = i - 1;  /* linear index -> (k % rows, k / rows) */
+        Pf[(size_t)row * (cols + 1) + i] = Pf[(size_t)row * (cols + 1) + i - 1] + pf[(size_t)(k % pf_rows) * cols + (k / pf_rows)];
+    }
+    Pf[(size_t)row * (cols + 1) + i] = 1;
+    return res;
+}
+static int env_build(Emitter *e, const nori_emitter_desc *d) {
+    int R = d->env_rows, C = d->env_cols;
+    if (R < 2 || C < 2 || !d->env_rgb) return NORI_ERR_INVALID;
+    e->R = R; e->C = C; e->weight = d->weight; e->rgb = d->env_rgb;
+    float *lum = (float *)malloc(sizeof(float) * (size_t)R * C);
+    float *sum = (float *)calloc((size_t)R, sizeof(float));
+    e->pdf = (float *)calloc((size_t)R * C, sizeof(float));
+    e->cdf = (float *)calloc((size_t)R * (C + 1), sizeof(float));
+    e->pmarg = (float *)calloc((size_t)R, sizeof(float));
+    e->cmarg = (float *)calloc((size_t)R + 1, sizeof(float));
+    for (int i = 0; i < R; i++)   /* envmap.cpp:42-50 */
+        for (int j = 0; j < C; j++) {
+            const float *c = &d->env_rgb[3 * ((size_t)i * C + j)];
+            lum[(size_t)i * C + j] = sqrtf((d->lum_scale[0] * c[0] + d->lum_scale[1] * c[1]) + d->lum_scale[2] * c[2]) +
+                                     EPS / 10000000;
+        }
+    for (int i = 0; i < R; ++i) sum[i] = env_precompute1D(i, lum, C, e->pdf, e->cdf, R);
+    env_precompute1D(0, sum, R, e->pmarg, e->cmarg, 1);
+    free(lum); free(sum);
+    return NORI_OK;
+}
+/* sphericalCoordinates (common.cpp:264-272) + mapIntersect (envmap.cpp:61-75) */
+static V2 env_map(const Emitter *e, V3 vec) {
+    float theta = acosf(vec.z), phi = atan2f(vec.y, vec.x);
+    if (phi < 0) phi = (float)((double)phi + 2 * M_PI);
+    V2 uv;
+    uv.x = theta * (float)(e->R - 1) * F_INV_PI;
+    uv.y = (float)((double)phi * 0.5 * (double)(e->C - 1) * (double)F_INV_PI);
+    if (isnan(uv.x) || isnan(uv.y)) { uv.x = 0; uv.y = 0; }
+    return uv;
+}
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline V3 env_texel(const Emitter *e, int i, int j) {
+    const float *c = &e->rgb[3 * ((size_t)i * e->C + j)];
+    return v3(c[0], c[1], c[2]);
+}
+/* EnvironmentMap::eval (envmap.cpp:124-156): bilinear, wrapping at the edges */
+static V3 env_eval(const Emitter *e, V3 wi) {
+    V2 uv = env_map(e, vnormalize(wi));
+    int u = clampi((int)uv.x, 0, e->R - 1), v = clampi((int)uv.y, 0, e->C - 1);
+    int us = (u + 1) % e->R, vs = (v + 1) % e->C;
+    V3 BL = env_texel(e, u, v), UL = env_texel(e, u, vs), BR = env_texel(e, us, v), UR = env_texel(e, us, vs);
+    int dusu = us - u, dvsv = vs - v;
+    float dusum = (float)us - uv.x, dumu = uv.x - (float)u, dvmv = uv.y - (float)v, dvsvm = (float)vs - uv.y;
+    V3 acc = vadd(vadd(vadd(vmuls(vmuls(BL, dusum), dvsvm), vmuls(vmuls(BR, dumu), dvsvm)), vmuls(vmuls(UL, dusum), dvmv)),
+                  vmuls(vmuls(UR, dumu), dvmv));
+    float inv = (float)(1.0 / (double)(dusu * dvsv));
+    V3 r = v3(inv * acc.x, inv * acc.y, inv * acc.z);
+    return v3(e->weight * r.x, e->weight * r.y, e->weight * r.z);
+}
+/* EnvironmentMap::pdf (envmap.cpp:184-192) */
+static float env_pdf(const Emitter *e, V3 wi) {
+    V2 uv = env_map(e, vnormalize(wi));
+    int i = clampi((int)uv.x, 0, e->R - 1), j = clampi((int)uv.y, 0, e->C - 1);
+    return e->pmarg[i] * e->pdf[(size_t)i * e->C + j];
+}
+/* sample1D (envmap.cpp:112-122); a row with no bracketing interval (an
+ * all-zero row) takes its last interval instead of reading out of bounds */
+static void env_sample1D(int row, const float *pf, const float *Pf, int cols, float s, float *x, float *prob) {
+    const float *P = Pf + (size_t)row * (cols + 1);
+    int i;
+    for (i = 0; i < cols; i++)
+        if (P[i] <= s && s < P[i + 1]) break;
+    if (i >= cols) i = cols - 1;
+    float t = (P[i + 1] - s) / (P[i + 1] - P[i]);
+    *x = (1 - t) * (float)i + t * (float)(i + 1);
+    *prob = pf[(size_t)row * cols + i];
+}
+/* EnvironmentMap::sample (envmap.cpp:158-181).  Deviation D4: the reference's
+ * Jacobian reads lRec.wi before it is set (uninitialised); the sampled
+ * direction is used here. */
+static V3 env_sample(const Emitter *e, V2 smp, V3 *wi) {
+    float u, v, u_pdf, v_pdf;
+    env_sample1D(0, e->pmarg, e->cmarg, e->R, smp.x, &u, &u_pdf);
+    env_sample1D((int)u, e->pdf, e->cdf, e->C, smp.y, &v, &v_pdf);
+    float theta = (float)((double)u * M_PI / (double)(e->R - 1));     /* invMapIntersect */
+    float phi = (float)((double)(v * 2.0f) * M_PI / (double)(e->C - 1));
+    *wi = vnormalize(v3(sinf(theta) * cosf(phi), sinf(theta) * sinf(phi), cosf(theta)));
+    float jac = (float)((double)((e->C - 1) * (e->R - 1)) / (2 * pow(M_PI, 2) * (double)sin_theta(*wi)));
+    v_pdf = env_pdf(e, *wi) * jac;
+    V3 c = env_eval(e, *wi);
+    return v3(c.x / v_pdf, c.y / v_pdf, c.z / v_pdf);
+}
+
 static inline V3 emitter_eval(const Emitter *e, const ERec *r) {
+    if (e->type == NORI_EMITTER_ENVMAP) return env_eval(e, r->wi);
     return vdot(r->n, vneg(r->wi)) > 0.0f ? e->radiance : v3(0, 0, 0);
 }
 static inline float emitter_pdf(const oracle_scene *s, const Emitter *e, const ERec *r) {
+    if (e->type == NORI_EMITTER_ENVMAP) return env_pdf(e, r->wi);
     float theta = vdot(r->n, vneg(r->wi));
     if (theta > 0.0f) return shape_pdf_surface(&s->shapes[e->shape]);
     return 0.0f;
 }
 static V3 emitter_sample(const oracle_scene *s, const Emitter *e, ERec *r, V2 smp) {
+    if (e->type == NORI_EMITTER_ENVMAP) {
+        V3 Li = env_sample(e, smp, &r->wi);
+        r->shadow = ray_make(r->ref, r->wi, EPS, ENV_T_FAR);
+        r->p = vadd(r->ref, vmuls(r->wi, ENV_T_FAR));  /* D4: lRec.p is never set by the reference */
+        r->n = vneg(r->wi);
+        r->pdf = env_pdf(e, r->wi);
+        return Li;
+    }
     shape_sample_surface(s, &s->shapes[e->shape], smp, &r->p, &r->n, &r->pdf);
     V3 d = vsub(r->p, r->ref);
     r->wi = vnormalize(d);
@@ -1233,7 +1353,9 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
     s->nemitters = d->num_emitters;
     s->emitters = (Emitter *)calloc(d->num_emitters ? d->num_emitters : 1, sizeof(Emitter));
     for (uint32_t i = 0; i < d->num_emitters; ++i) {
-        if (d->emitters[i].type != NORI_EMITTER_AREA) { oracle_scene_free(s); return NORI_ERR_UNSUPPORTED; }
+        if (d->emitters[i].type == NORI_EMITTER_ENVMAP) {
+            if (env_build(&s->emitters[i], &d->emitters[i]) != NORI_OK) { oracle_scene_free(s); return NORI_ERR_INVALID; }
+        } else if (d->emitters[i].type != NORI_EMITTER_AREA) { oracle_scene_free(s); return NORI_ERR_UNSUPPORTED; }
         s->emitters[i].type = d->emitters[i].type;
         s->emitters[i].shape = d->emitters[i].shape;
         s->emitters[i].radiance = v3(d->emitters[i].radiance[0], d->emitters[i].radiance[1], d->emitters[i].radiance[2]);
@@ -1274,6 +1396,9 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
 void oracle_scene_free(oracle_scene *s) {
     if (!s) return;
     for (uint32_t i = 0; i < s->nshapes; ++i) free(s->shapes[i].cdf);
+    for (uint32_t i = 0; s->emitters && i < s->nemitters; ++i) {
+        free(s->emitters[i].pdf); free(s->emitters[i].cdf); free(s->emitters[i].pmarg); free(s->emitters[i].cmarg);
+    }
     free(s->shapes); free(s->shape_offset); free(s->bsdfs); free(s->emitters);
     free(s->nodes); free(s->indices);
     free(s);

@@ -68,3 +68,57 @@ def heightfield_scene(outdir, n=64, integrator="path_mis", width=256, height=256
 </scene>
 """)
     return xml
+
+
+DISNEY = os.path.join(os.path.dirname(HERE), "scenes", "project", "disney")
+
+
+def envmap_image(rows=256, cols=512):
+    """Lat-long HDR map of fixed formula (the reference's envmaptext.exr / sky.exr
+    are missing): rows index theta in [0, pi] (the envmap's `m_width` axis),
+    cols index phi in [0, 2 pi).  Sky gradient + a sun lobe + a warm horizon band."""
+    th = (np.arange(rows, dtype=np.float64) + 0.5) / rows * np.pi
+    ph = (np.arange(cols, dtype=np.float64) + 0.5) / cols * 2 * np.pi
+    T, P = np.meshgrid(th, ph, indexing="ij")
+    d = np.stack([np.sin(T) * np.cos(P), np.sin(T) * np.sin(P), np.cos(T)], -1)
+    sun = np.array([0.3, 0.5, 0.81])
+    sun /= np.linalg.norm(sun)
+    lobe = np.exp(40.0 * (d @ sun - 1.0))
+    sky = 0.4 + 0.6 * np.clip(np.cos(T), 0, 1)
+    band = np.exp(-((T - np.pi / 2) / 0.15) ** 2)
+    img = np.stack([0.35 * sky + 0.8 * band + 30 * lobe,
+                    0.55 * sky + 0.5 * band + 28 * lobe,
+                    0.95 * sky + 0.2 * band + 24 * lobe], -1)
+    return img.astype(np.float32)
+
+
+def envmap_scene(outdir, width=128, height=128, spp=16, integrator="path_mis", rows=256, cols=512, radius=30.0):
+    """Config C4: the Disney-sphere Cornell box of
+    scenes/project/disney inside an env-mapped sky sphere, as in the reference's
+    scenes/project/envmap.xml pattern (envmap emitter on a radius-30 sphere)."""
+    import nori_amd
+
+    os.makedirs(outdir, exist_ok=True)
+    exr = os.path.join(outdir, f"sky_{rows}x{cols}.exr")
+    if not os.path.exists(exr):
+        nori_amd.write_exr(exr, envmap_image(rows, cols))
+    src = open(os.path.join(DISNEY, "cbox_path_mis.xml")).read()
+    src = src.replace('value="meshes/', f'value="{os.path.join(DISNEY, "meshes")}/')
+    src = src.replace('<integrator type="path_mis"/>', f'<integrator type="{integrator}"/>')
+    src = src.replace('<integer name="height" value="600"/>', f'<integer name="height" value="{height}"/>')
+    src = src.replace('<integer name="width" value="800"/>', f'<integer name="width" value="{width}"/>')
+    src = src.replace('<integer name="sampleCount" value="1024"/>', f'<integer name="sampleCount" value="{spp}"/>')
+    sky = f"""
+	<mesh type="sphere">
+		<point name="center" value="0,1,0"/>
+		<float name="radius" value="{radius}"/>
+		<emitter type="envmap">
+			<string name="filename" value="{exr}"/>
+		</emitter>
+	</mesh>
+</scene>"""
+    src = src.replace("</scene>", sky)
+    xml = os.path.join(outdir, f"envmap_{integrator}.xml")
+    with open(xml, "w") as f:
+        f.write(src)
+    return xml
