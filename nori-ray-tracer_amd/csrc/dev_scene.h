@@ -117,7 +117,10 @@ struct ShadowQueue {
 // static stream of 256-id chunks (consecutive ids = adjacent pixels of one
 // 32x32 block, so a segment traces coherent camera rays).
 constexpr uint32_t kSeg = 256;
-constexpr uint32_t kScanGroup = 4;  // triangles fetched per batch of scalar loads in the scan
+#ifndef NORI_SCAN_GROUP
+#define NORI_SCAN_GROUP 4
+#endif
+constexpr uint32_t kScanGroup = NORI_SCAN_GROUP;  // triangles fetched per batch of scalar loads in the scan
 struct WorkDesc {
     uint64_t total;          // work ids in this chunk of passes
     uint32_t M;              // pixels in the selected blocks

@@ -14,7 +14,7 @@ constexpr int kTraceBlock = 128;   // traversal work-group size (LDS stack colum
 constexpr int kTraceGroup = NORI_TRACE_GROUP;  // segments per extend/shadow work-group
 constexpr int kSplatBlock = 256;
 #ifndef NORI_SCAN_RAYS
-#define NORI_SCAN_RAYS 2
+#define NORI_SCAN_RAYS 1
 #endif
 constexpr int kScanRays = NORI_SCAN_RAYS;  // rays per thread of the scan-mode trace kernels
 #ifndef NORI_SHADE_LDS_MAX

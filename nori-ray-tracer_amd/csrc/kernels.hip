@@ -1255,8 +1255,11 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
 #pragma unroll
             for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = acc[a][c][2] = acc[a][c][3] = 0.0f;
         bool any = false;
+        // the next pass's record is in flight while this one is splatted
+        float4 Ln = p0 < p1 ? rec[(size_t)p0 * sd.M + off + j] : make_float4(0, 0, 0, 1);
         for (uint32_t p = p0; p < p1; ++p) {
-            float4 L = rec[(size_t)p * sd.M + off + j];
+            const float4 L = Ln;
+            if (p + 1 < p1) Ln = rec[(size_t)(p + 1) * sd.M + off + j];
             if (L.w != 0.0f) continue;  // pending: the finisher splats this sample
             uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
             Pcg r;
@@ -1278,17 +1281,25 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
                 int cx = lx + d, cy = ly + d;  // tile column / row of window cell d
                 int kx = min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION);
                 int ky = min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION);
-                wx[d] = (cx >= x0 && cx <= x1) ? ftab[kx] : 0.0f;
-                wy[d] = (cy >= y0 && cy <= y1) ? ftab[ky] : 0.0f;
+                const float fx = ftab[kx], fy = ftab[ky];  // unconditional: no branch per cell
+                wx[d] = (cx >= x0 && cx <= x1) ? fx : 0.0f;
+                wy[d] = (cy >= y0 && cy <= y1) ? fy : 0.0f;
+            }
+            float lx_[K], ly_[K], lz_[K];  // Color4f(value) * wx (the row factor is shared by all rows)
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                lx_[c] = L.x * wx[c];
+                ly_[c] = L.y * wx[c];
+                lz_[c] = L.z * wx[c];
             }
 #pragma unroll
             for (int a = 0; a < K; ++a)
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    acc[a][c][0] += (L.x * wx[c]) * wy[a];
-                    acc[a][c][1] += (L.y * wx[c]) * wy[a];
-                    acc[a][c][2] += (L.z * wx[c]) * wy[a];
-                    acc[a][c][3] += (1.0f * wx[c]) * wy[a];
+                    acc[a][c][0] += lx_[c] * wy[a];
+                    acc[a][c][1] += ly_[c] * wy[a];
+                    acc[a][c][2] += lz_[c] * wy[a];
+                    acc[a][c][3] += wx[c] * wy[a];  // (1 * wx) * wy
                 }
         }
         if (any) {

@@ -543,6 +543,11 @@ bool debug_log() {
     const char *e = std::getenv("NORI_DEBUG");
     return e && e[0] == '1';
 }
+uint64_t event_every() {  // NORI_EVENT_EVERY: iterations per host event (default 1)
+    const char *e = std::getenv("NORI_EVENT_EVERY");
+    const long v = e ? std::atol(e) : 1;
+    return v >= 1 && v <= 8 ? (uint64_t)v : 1;
+}
 bool fused_extend() {
     const char *e = std::getenv("NORI_FUSED_EXTEND");
     return e && e[0] == '1';
@@ -643,6 +648,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // NORI_FUSED_EXTEND=1: scan-mode scenes trace the extension rays inside
     // the shade kernel (measured even with separate k_extend launches)
     const bool fused = c.stack == 0 && fused_extend();
+    const uint64_t every = event_every();
     const uint32_t G = pool / kSeg;
     SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
                  c.segstats.as<uint4>()};
@@ -671,11 +677,16 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             });
             if (!fused) timed(0, [&] { return launch_extend(S, Q[out], seg.cnt[out], G, c.stack, c.stream); });
             timed(1, [&] { return launch_shadow(S, sq, seg.shcnt, c.rec.as<float4>(), G, c.stack, c.stream); });
-            HIP_TRY(hipEventRecord(c.ring[it % kRing], c.stream));
             ++iters;
-            if (it >= (uint64_t)kLookahead) {
-                // bound the run-ahead of the host to kLookahead iterations
-                HIP_TRY(hipEventSynchronize(c.ring[(it - kLookahead) % kRing]));
+            // an event every `every` iterations (each record adds a gap
+            // between dependent kernels); the host waits on the one from at
+            // least kLookahead iterations back
+            if ((it + 1) % every != 0) continue;
+            const uint64_t ev = it / every;
+            HIP_TRY(hipEventRecord(c.ring[ev % kRing], c.stream));
+            const uint64_t lag = (kLookahead + every - 1) / every;
+            if (ev >= lag) {
+                HIP_TRY(hipEventSynchronize(c.ring[(ev - lag) % kRing]));
                 uint32_t exhausted = __atomic_load_n(&c.pinned[1], __ATOMIC_ACQUIRE);
                 c.progress = (float)std::min(1.0, (double)done_before / (double)total_all +
                                                       (double)np / passes * exhausted / G);
