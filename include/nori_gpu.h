@@ -21,6 +21,7 @@
  *   nori_film_develop     <- ImageBlock::toBitmap         src/block.cpp:76-82
  *   nori_write_exr        <- Bitmap::save                 src/bitmap.cpp:82-107
  *   nori_read_exr         <- Bitmap::Bitmap(filename)     src/bitmap.cpp:23-80
+ *   nori_scene_bvh_info   <- BVH::build/statistics        src/bvh.cpp:329-402
  *
  * Rules of the ABI: plain C types only, no exceptions cross it, every call
  * returns an int status (NORI_OK = 0, negative = error) and the message of
@@ -175,6 +176,21 @@ int nori_write_exr(const char *path, const float *rgb, int width, int height);
  * FLOAT) <- Bitmap::Bitmap (bitmap.cpp:23-80).  Call with rgb = NULL to get
  * the size, then with a buffer of 3*width*height floats (row-major). */
 int nori_read_exr(const char *path, int *width, int *height, float *rgb);
+
+/* Host-side BVH build of the scene exactly as nori_gpu_create builds it (no
+ * device needed) <- BVH::build + BVH::statistics (bvh.cpp:329-402): node count
+ * and SAH cost of the reference-layout tree, device node count and depth, and
+ * an FNV-1a hash of the leaf-order primitive ids. */
+typedef struct nori_bvh_info {
+    uint32_t ref_nodes;       /* nodes reachable in the reference layout      */
+    uint32_t device_nodes;    /* 64-byte inner nodes of the device layout     */
+    uint32_t depth;           /* inner-node depth of the device tree          */
+    uint32_t num_prims;
+    float sah_cost;           /* BVH::statistics cost of the root             */
+    uint32_t pad;
+    uint64_t order_hash;      /* FNV-1a over the leaf-order primitive ids     */
+} nori_bvh_info;
+int nori_scene_bvh_info(const nori_scene_desc *scene, nori_bvh_info *out);
 
 /* ---- GPU context ----------------------------------------------------------- */
 typedef struct nori_gpu_ctx nori_gpu_ctx;

@@ -12,6 +12,8 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <thread>
+#include <vector>
 
 #include "host_scene.h"
 
@@ -60,6 +62,9 @@ struct RefNode {  // bvh.h:127-164 semantics
     uint32_t b = 0;  // leaf: start | inner: right child
     Box box;
 };
+
+constexpr int kParDepth = 5;          // up to 2^5 concurrent subtree builds
+constexpr uint32_t kParMin = 16384;   // smallest subtree given its own thread
 
 struct Builder {
     std::vector<RefNode> nodes;
@@ -116,7 +121,18 @@ struct Builder {
         serial(l, start, start + lc, tmp);
         serial(r, start + lc, end, tmp + lc);
     }
-    void task(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp) {  // bvh.cpp:100-233
+    // bvh.cpp:100-233.  Subtrees own disjoint index, scratch and node ranges
+    // (the left subtree of a node with lc primitives gets nodes ni+1 ..
+    // ni+2lc-1), so large right subtrees are built on their own threads --
+    // the reference's tbb::task tree -- with a result independent of scheduling.
+    void task(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp, int depth = 0) {
+        std::vector<std::thread> kids;
+        struct Join {
+            std::vector<std::thread> &k;
+            ~Join() {
+                for (auto &t : k) t.join();
+            }
+        } join{kids};
         for (;;) {
             uint32_t size = (uint32_t)(end - start);
             RefNode &node = nodes[ni];
@@ -174,9 +190,16 @@ struct Builder {
                 else tmp[ir++] = f;
             }
             std::memcpy(start, tmp, size * sizeof(uint32_t));
-            task(r, start + lc, end, tmp + lc);
+            if (depth < kParDepth && size - lc >= kParMin) {
+                uint32_t *s2 = start + lc, *e2 = end, *t2 = tmp + lc;
+                const int d2 = depth + 1;
+                kids.emplace_back([this, r, s2, e2, t2, d2] { task(r, s2, e2, t2, d2); });
+            } else {
+                task(r, start + lc, end, tmp + lc, depth + 1);
+            }
             ni = l;
             end = start + lc;
+            ++depth;
         }
     }
     float statistics(uint32_t ni, uint32_t &count) const {  // bvh.cpp:384-402

@@ -228,6 +228,30 @@ template <class F> int guarded(F &&f) {
     }
 }
 
+// Scene box = BVH root box: every mesh vertex and every sphere's bounds.
+void scene_root_box(const nori_scene_desc &d, float rmin[3], float rmax[3]) {
+    for (int k = 0; k < 3; ++k) rmin[k] = __builtin_inff(), rmax[k] = -__builtin_inff();
+    auto expand = [&](float x, float y, float z) {
+        float p[3] = {x, y, z};
+        for (int k = 0; k < 3; ++k) {
+            rmin[k] = std::fmin(rmin[k], p[k]);
+            rmax[k] = std::fmax(rmax[k], p[k]);
+        }
+    };
+    for (uint32_t s = 0; s < d.num_shapes; ++s) {
+        const nori_shape_desc &sd = d.shapes[s];
+        if (sd.type == NORI_SHAPE_SPHERE) {
+            expand(sd.center[0] - sd.radius, sd.center[1] - sd.radius, sd.center[2] - sd.radius);
+            expand(sd.center[0] + sd.radius, sd.center[1] + sd.radius, sd.center[2] + sd.radius);
+        } else {
+            for (uint32_t v = 0; v < sd.vtx_count; ++v) {
+                const float *p = d.positions + 3 * (size_t)(sd.vtx_offset + v);
+                expand(p[0], p[1], p[2]);
+            }
+        }
+    }
+}
+
 void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     float rmin[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float rmax[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
@@ -791,6 +815,31 @@ int nori_scene_load_xml(const char *path, int width, int height, int spp, nori_s
     });
 }
 const nori_scene_desc *nori_scene_get_desc(const nori_scene *s) { return s ? &s->hs->desc : nullptr; }
+
+int nori_scene_bvh_info(const nori_scene_desc *d, nori_bvh_info *out) {
+    return guarded([&] {
+        if (!d || !out) return fail(NORI_ERR_INVALID, "null argument");
+        if (d->abi_version != NORI_GPU_ABI_VERSION) return fail(NORI_ERR_INVALID, "ABI version mismatch");
+        float rmin[3], rmax[3];
+        scene_root_box(*d, rmin, rmax);
+        DeviceBvh bvh;
+        build_device_bvh(*d, rmin, rmax, bvh);
+        std::memset(out, 0, sizeof(*out));
+        out->ref_nodes = bvh.ref_nodes;
+        out->device_nodes = bvh.num_nodes;
+        out->depth = bvh.depth;
+        out->num_prims = (uint32_t)(bvh.prims.size() / 12);
+        out->sah_cost = bvh.sah_cost;
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < bvh.prims.size(); i += 12) {
+            uint32_t id;
+            std::memcpy(&id, &bvh.prims[i + 3], 4);
+            for (int k = 0; k < 4; ++k) h = (h ^ ((id >> (8 * k)) & 0xFFu)) * 1099511628211ull;
+        }
+        out->order_hash = h;
+        return NORI_OK;
+    });
+}
 void nori_scene_free(nori_scene *s) { delete s; }
 
 int nori_film_border(const nori_scene_desc *d) { return d ? film_border(d->camera) : NORI_ERR_INVALID; }

@@ -127,6 +127,18 @@ def write_exr(path, rgb):
     check(lib().nori_write_exr(os.fsencode(path), _fptr(rgb), rgb.shape[1], rgb.shape[0]))
 
 
+class BvhInfo(C.Structure):
+    _fields_ = [("ref_nodes", C.c_uint32), ("device_nodes", C.c_uint32), ("depth", C.c_uint32),
+                ("num_prims", C.c_uint32), ("sah_cost", C.c_float), ("pad", C.c_uint32), ("order_hash", C.c_uint64)]
+
+
+def bvh_info(scene):
+    """Host build of the scene's BVH as the GPU context builds it (nori_scene_bvh_info)."""
+    info = BvhInfo()
+    check(lib().nori_scene_bvh_info(scene.desc_ptr, C.byref(info)))
+    return {k: getattr(info, k) for k, _ in BvhInfo._fields_ if k != "pad"}
+
+
 def read_exr(path):
     """R, G, B planes of an OpenEXR file as a (height, width, 3) float32 array (nori_read_exr)."""
     w, h = C.c_int(), C.c_int()

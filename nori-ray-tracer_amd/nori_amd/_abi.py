@@ -106,6 +106,7 @@ SIGNATURES = {
     "nori_film_develop": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "nori_write_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, C.c_int]),
     "nori_read_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)]),
+    "nori_scene_bvh_info": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nori_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nori_gpu_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "nori_gpu_render": (C.c_int, [C.c_void_p, C.POINTER(RenderDesc), C.c_void_p, C.POINTER(Stats)]),

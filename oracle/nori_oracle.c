@@ -29,6 +29,7 @@
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #include <time.h>
 #include <unistd.h>
@@ -426,7 +427,12 @@ static inline void bbox_expand_p(BBox *b, V3 p) {
     b->min = v3(fminf(b->min.x, p.x), fminf(b->min.y, p.y), fminf(b->min.z, p.z));
     b->max = v3(fmaxf(b->max.x, p.x), fmaxf(b->max.y, p.y), fmaxf(b->max.z, p.z));
 }
-static inline void bbox_expand(BBox *b, const BBox *o) { bbox_expand_p(b, o->min); bbox_expand_p(b, o->max); }
+/* BoundingBox::expandBy(const BoundingBox &) (bbox.h:294-297): component-wise
+ * min of the mins and max of the maxes, so an empty box is neutral */
+static inline void bbox_expand(BBox *b, const BBox *o) {
+    b->min = v3(fminf(b->min.x, o->min.x), fminf(b->min.y, o->min.y), fminf(b->min.z, o->min.z));
+    b->max = v3(fmaxf(b->max.x, o->max.x), fmaxf(b->max.y, o->max.y), fmaxf(b->max.z, o->max.z));
+}
 static inline float bbox_area(const BBox *b) { /* bbox.h:87-100 */
     float d[3] = {b->max.x - b->min.x, b->max.y - b->min.y, b->max.z - b->min.z};
     float result = 0.0f;
@@ -1404,6 +1410,25 @@ void oracle_scene_free(oracle_scene *s) {
     free(s);
 }
 uint32_t oracle_scene_node_count(const oracle_scene *s) { return s ? s->nnodes : 0; }
+/* BVH::statistics (bvh.cpp:384-402) over the tree reachable from the root */
+static float bvh_statistics(const oracle_scene *s, uint32_t ni, uint32_t *count) {
+    const Node *n = &s->nodes[ni];
+    if (n->flag_size & 1u) { *count = 1; return (float)(n->flag_size >> 1); }
+    uint32_t cl, cr;
+    float sl = bvh_statistics(s, ni + 1, &cl), sr = bvh_statistics(s, n->start_right, &cr);
+    *count = cl + cr + 1;
+    return 2 + (bbox_area(&s->nodes[ni + 1].bbox) * sl + bbox_area(&s->nodes[n->start_right].bbox) * sr) /
+               bbox_area(&n->bbox);
+}
+int oracle_scene_bvh_stats(const oracle_scene *s, uint32_t *nodes, float *sah, uint64_t *order_hash) {
+    if (!s || !s->nnodes) return NORI_ERR_INVALID;
+    *sah = bvh_statistics(s, 0, nodes);
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t i = 0; i < s->nprims; ++i)
+        for (int k = 0; k < 4; ++k) h = (h ^ ((s->indices[i] >> (8 * k)) & 0xFFu)) * 1099511628211ull;
+    *order_hash = h;
+    return NORI_OK;
+}
 
 /* ------------------------------------------------------------------ render */
 typedef struct {

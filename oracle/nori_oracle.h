@@ -38,6 +38,8 @@ typedef struct oracle_stats {
 int oracle_scene_create(const nori_scene_desc *desc, oracle_scene **out);
 void oracle_scene_free(oracle_scene *s);
 uint32_t oracle_scene_node_count(const oracle_scene *s);
+/* reachable node count and BVH::statistics cost of the tree, FNV-1a hash of the leaf-order primitive ids */
+int oracle_scene_bvh_stats(const oracle_scene *s, uint32_t *nodes, float *sah, uint64_t *order_hash);
 
 /* render.cpp:173-250 pass loop.  Adds into rgbw ((H+2b)x(W+2b)x4).
  * rng_mode: NORI_RNG_WAVE or NORI_RNG_BLOCK.  nthreads<=0: all hw threads.

@@ -44,6 +44,7 @@ def lib():
             "oracle_scene_create": (C.c_int, [vp, C.POINTER(vp)]),
             "oracle_scene_free": (None, [vp]),
             "oracle_scene_node_count": (u32, [vp]),
+            "oracle_scene_bvh_stats": (C.c_int, [vp, C.POINTER(u32), C.POINTER(C.c_float), C.POINTER(u64)]),
             "oracle_render": (C.c_int, [vp, C.c_int, u64, u32, u32, C.POINTER(u32), u32, C.c_int, C.c_int, pf,
                                         C.POINTER(OracleStats)]),
             "oracle_trace": (C.c_int, [vp, pf, u32, C.c_int, vp]),
@@ -152,6 +153,14 @@ class OracleScene:
 
     def node_count(self):
         return lib().oracle_scene_node_count(self._h)
+
+    def bvh_stats(self):
+        """(reachable nodes, BVH::statistics SAH cost, FNV-1a hash of the leaf-order primitive ids)."""
+        n, sah, h = C.c_uint32(), C.c_float(), C.c_uint64()
+        rc = lib().oracle_scene_bvh_stats(self._h, C.byref(n), C.byref(sah), C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"oracle_scene_bvh_stats: {rc}")
+        return n.value, sah.value, h.value
 
 
 def bsdf_ttest(bsdf_desc, angle_deg, n=100000):
