@@ -9,6 +9,9 @@
 // child boxes stored in the parent so one 64-byte fetch tests both children,
 // leaves inlined into the child reference.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -65,10 +68,12 @@ struct RefNode {  // bvh.h:127-164 semantics
 
 constexpr int kParDepth = 5;          // up to 2^5 concurrent subtree builds
 constexpr uint32_t kParMin = 16384;   // smallest subtree given its own thread
+constexpr uint32_t kPresortMin = 256; // serial sweeps at least this large keep presorted axis orders
 
 struct Builder {
     std::vector<RefNode> nodes;
     std::vector<uint32_t> idx, temp;
+    std::vector<uint8_t> side;  // per primitive: left/right of the split being partitioned
     std::vector<float> cent;  // 3 per prim
     std::vector<Box> pbox;
 
@@ -80,7 +85,29 @@ struct Builder {
             return a < b;
         });
     }
-    void serial(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp) {  // bvh.cpp:236-305
+    // bvh.cpp:236-305: full-sweep SAH over the three axis orders of the node.
+    // Small nodes re-sort their range per axis like the reference; large ones
+    // (the reference falls back here when binning finds no split, e.g. a
+    // 250k-triangle node next to the Cornell-box walls, and then peels a few
+    // primitives off per level) keep all three orders sorted from the top and
+    // stably partition them at each split: a stable partition of a sorted list
+    // is the sorted list of the part, so the tree is identical without the
+    // O(n log n) re-sort per level.
+    void serial(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp, int depth = 0) {
+        const uint32_t size = (uint32_t)(end - start);
+        if (size < kPresortMin) {
+            serial_small(ni, start, end, tmp);
+            return;
+        }
+        std::vector<uint32_t> ord(3 * (size_t)size), scratch(size);
+        uint32_t *o[3] = {ord.data(), ord.data() + size, ord.data() + 2 * (size_t)size};
+        for (int a = 0; a < 3; ++a) {
+            std::memcpy(o[a], start, size * sizeof(uint32_t));
+            sort_axis(o[a], size, a);
+        }
+        sweep(ni, start, o, size, scratch.data(), depth);
+    }
+    void serial_small(uint32_t ni, uint32_t *start, uint32_t *end, uint32_t *tmp) {
         RefNode &node = nodes[ni];
         node.used = true;
         uint32_t size = (uint32_t)(end - start);
@@ -118,8 +145,74 @@ struct Builder {
         node.leaf = false;
         node.a = (uint32_t)best_axis;
         node.b = r;
-        serial(l, start, start + lc, tmp);
-        serial(r, start + lc, end, tmp + lc);
+        serial_small(l, start, start + lc, tmp);
+        serial_small(r, start + lc, end, tmp + lc);
+    }
+    // o[a]: the node's primitives sorted along axis a (ties by id); out: the
+    // node's range of the final index array; la: `size` words of scratch.
+    void sweep(uint32_t ni, uint32_t *out, uint32_t *const o[3], uint32_t size, uint32_t *la, int depth) {
+        if (size < kPresortMin) {  // small enough: back to the plain form on the z-sorted range
+            std::memcpy(out, o[2], size * sizeof(uint32_t));
+            serial_small(ni, out, out + size, la);
+            return;
+        }
+        RefNode &node = nodes[ni];
+        node.used = true;
+        float best_cost = (float)1 * size;
+        int64_t best_index = -1, best_axis = -1;
+        float *left_areas = reinterpret_cast<float *>(la);
+        for (int axis = 0; axis < 3; ++axis) {
+            const uint32_t *s = o[axis];
+            Box bb;
+            for (uint32_t i = 0; i < size; ++i) {
+                bb.expand(pbox[s[i]]);
+                left_areas[i] = bb.area();
+            }
+            if (axis == 0) node.box = bb;
+            bb = Box();
+            float tri_factor = 1 / node.box.area();
+            for (uint32_t i = size - 1; i >= 1; --i) {
+                bb.expand(pbox[s[i]]);
+                float sah = 2.0f * 1 + tri_factor * ((float)i * left_areas[i - 1] + (float)(size - i) * bb.area());
+                if (sah < best_cost) {
+                    best_cost = sah;
+                    best_index = i;
+                    best_axis = axis;
+                }
+            }
+        }
+        if (best_index == -1) {  // leaf: the reference leaves its range sorted along z
+            std::memcpy(out, o[2], size * sizeof(uint32_t));
+            node.leaf = true;
+            node.a = size;
+            node.b = (uint32_t)(out - idx.data());
+            return;
+        }
+        const uint32_t lc = (uint32_t)best_index, l = ni + 1, r = ni + 2 * lc;
+        node.leaf = false;
+        node.a = (uint32_t)best_axis;
+        node.b = r;
+        const uint32_t *sb = o[best_axis];
+        for (uint32_t i = 0; i < size; ++i) side[sb[i]] = i < lc ? 0 : 1;
+        for (int a = 0; a < 3; ++a) {
+            if (a == best_axis) continue;
+            uint32_t il = 0, ir = lc;
+            for (uint32_t i = 0; i < size; ++i) {
+                const uint32_t f = o[a][i];
+                if (side[f] == 0) la[il++] = f;
+                else la[ir++] = f;
+            }
+            std::memcpy(o[a], la, size * sizeof(uint32_t));
+        }
+        uint32_t *ol[3] = {o[0], o[1], o[2]}, *orr[3] = {o[0] + lc, o[1] + lc, o[2] + lc};
+        if (depth < kParDepth && size - lc >= kParMin && lc >= kParMin) {
+            std::thread t([this, r, out, lc, orr, size, la, depth] { sweep(r, out + lc, orr, size - lc, la + lc, depth + 1); });
+            sweep(l, out, ol, lc, la, depth + 1);
+            t.join();
+        } else {
+            sweep(l, out, ol, lc, la, depth + 1);
+            sweep(r, out + lc, orr, size - lc, la + lc, depth + 1);
+        }
     }
     // bvh.cpp:100-233.  Subtrees own disjoint index, scratch and node ranges
     // (the left subtree of a node with lc primitives gets nodes ni+1 ..
@@ -138,7 +231,7 @@ struct Builder {
             RefNode &node = nodes[ni];
             node.used = true;
             if (size < 32) {
-                serial(ni, start, end, tmp);
+                serial(ni, start, end, tmp, depth);
                 return;
             }
             int axis = node.box.largest_axis();
@@ -173,7 +266,7 @@ struct Builder {
                 right.expand(bins[i]);
             }
             if (best_index == -1) {
-                serial(ni, start, end, tmp);
+                serial(ni, start, end, tmp, depth);
                 return;
             }
             uint32_t lc = counts[best_index], l = ni + 1, r = ni + 2 * lc;
@@ -232,6 +325,13 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     out = DeviceBvh();
     if (n == 0) throw NoriException(NORI_ERR_INVALID, "scene has no primitives");
     if (n >= (1u << 25)) throw NoriException(NORI_ERR_UNSUPPORTED, "more than 2^25 primitives");
+    auto T0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!std::getenv("NORI_DEBUG")) return;
+        auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[nori] bvh %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - T0).count());
+        T0 = t;
+    };
     Builder b;
     b.cent.resize(3 * (size_t)n);
     b.pbox.resize(n);
@@ -256,12 +356,16 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     b.nodes.assign(2 * (size_t)n, RefNode());
     b.idx.resize(n);
     b.temp.resize(n);
+    b.side.assign(n, 0);
     for (uint32_t i = 0; i < n; ++i) b.idx[i] = i;
     for (int k = 0; k < 3; ++k) b.nodes[0].box.mn[k] = root_min[k], b.nodes[0].box.mx[k] = root_max[k];
+    lap("setup");
     b.task(0, b.idx.data(), b.idx.data() + n, b.temp.data());
+    lap("build");
     uint32_t cnt = 0;
     out.sah_cost = b.statistics(0, cnt);
     out.ref_nodes = cnt;
+    lap("statistics");
 
     // ---- primitive records in leaf order
     out.prims.assign(12 * (size_t)n, 0.0f);
@@ -360,6 +464,7 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     }
     out.num_nodes = (uint32_t)(nodes.size() / 16);
     out.depth = max_depth;
+    lap("device layout");
 }
 
 }  // namespace nori
