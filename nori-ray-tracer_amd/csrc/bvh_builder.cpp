@@ -462,8 +462,68 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     } else {
         emit(0, 0);
     }
-    out.num_nodes = (uint32_t)(nodes.size() / 16);
-    out.depth = max_depth;
+    // ---- collapse the binary device tree into the 4-wide layout
+    std::vector<float> bin;
+    bin.swap(nodes);
+    struct C4 {
+        uint32_t ref;
+        float mn[3], mx[3];
+    };
+    auto kids = [&](uint32_t n, C4 c[2]) {
+        const float *nd = &bin[16 * (size_t)n];
+        for (int k = 0; k < 3; ++k) {
+            c[0].mn[k] = nd[k];
+            c[0].mx[k] = nd[4 + k];
+            c[1].mn[k] = nd[8 + k];
+            c[1].mx[k] = nd[12 + k];
+        }
+        std::memcpy(&c[0].ref, &nd[3], 4);
+        std::memcpy(&c[1].ref, &nd[7], 4);
+    };
+    auto area = [](const C4 &c) {
+        float d[3] = {c.mx[0] - c.mn[0], c.mx[1] - c.mn[1], c.mx[2] - c.mn[2]};
+        return 2.0f * ((d[0] * d[1] + d[1] * d[2]) + d[2] * d[0]);
+    };
+    auto empty = [](const C4 &c) { return c.mn[0] > c.mx[0] || c.mn[1] > c.mx[1] || c.mn[2] > c.mx[2]; };
+    uint32_t depth4 = 0;
+    std::function<uint32_t(uint32_t, uint32_t)> collapse = [&](uint32_t n, uint32_t depth) -> uint32_t {
+        C4 two[2];
+        kids(n, two);
+        std::vector<C4> ch(two, two + 2);
+        while (ch.size() < 4) {  // open the inner child of largest area (DFS order kept)
+            int best = -1;
+            float ba = -1.0f;
+            for (size_t i = 0; i < ch.size(); ++i)
+                if (!(ch[i].ref & kLeafBit) && !empty(ch[i]) && area(ch[i]) > ba) {
+                    ba = area(ch[i]);
+                    best = (int)i;
+                }
+            if (best < 0) break;
+            kids(ch[(size_t)best].ref, two);
+            ch[(size_t)best] = two[0];
+            ch.insert(ch.begin() + best + 1, two[1]);
+        }
+        const uint32_t me = (uint32_t)(nodes.size() / 32);
+        nodes.resize(nodes.size() + 32, 0.0f);
+        depth4 = std::max(depth4, depth + 1);
+        uint32_t refs[4];
+        for (int i = 0; i < 4; ++i) {
+            const bool use = (size_t)i < ch.size() && !empty(ch[(size_t)i]);
+            refs[i] = use ? ch[(size_t)i].ref : kLeafBit;  // unused: NaN box, never entered
+            if (use && !(refs[i] & kLeafBit)) refs[i] = collapse(refs[i], depth + 1);
+            float *nd = &nodes[32 * (size_t)me];
+            for (int k = 0; k < 3; ++k) {
+                nd[4 * k + i] = use ? ch[(size_t)i].mn[k] : __builtin_nanf("");
+                nd[4 * (3 + k) + i] = use ? ch[(size_t)i].mx[k] : __builtin_nanf("");
+            }
+        }
+        std::memcpy(&nodes[32 * (size_t)me + 24], refs, 16);
+        return me;
+    };
+    collapse(0, 0);
+    out.num_nodes = (uint32_t)(nodes.size() / 32);
+    out.depth = depth4;
+    (void)max_depth;
     lap("device layout");
 }
 

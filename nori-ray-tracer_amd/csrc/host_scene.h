@@ -55,23 +55,25 @@ HostScene *load_scene_xml(const std::string &path, int width, int height, int sp
 int load_exr(const std::string &path, int &width, int &height, std::vector<float> &rgb);
 
 // ---- BVH in device layout -------------------------------------------------
-// Inner node = 4 x float4 (64 B, one cache line):
-//   [0] left  child box min.xyz, left  child ref
-//   [1] left  child box max.xyz, right child ref
-//   [2] right child box min.xyz, 0
-//   [3] right child box max.xyz, 0
-// A child ref with bit 31 clear is an inner-node index; with bit 31 set it is
-// a leaf: bits 0-24 first primitive record, bits 25-30 count-1 (<= 64 prims).
+// The reference's binary tree is collapsed into a 4-wide tree (each node takes
+// the inner children of largest surface area apart until it holds 4).  Inner
+// node = 8 x float4 (128 B), children in SoA form:
+//   [0] min.x of children 0..3  [1] min.y  [2] min.z
+//   [3] max.x                   [4] max.y  [5] max.z
+//   [6] child refs (uint bits)  [7] unused
+// Unused child slots have NaN boxes (every slab test fails).  A child ref with
+// bit 31 clear is an inner-node index; with bit 31 set it is a leaf: bits 0-24
+// first primitive record, bits 25-30 count-1 (<= 64 prims).
 // Primitive record = 3 x float4 (48 B), in leaf order:
 //   triangle: (v0.xyz, prim id), (e1.xyz, 0), (e2.xyz, 0)   e1=p1-p0, e2=p2-p0
 //   sphere  : (center.xyz, prim id), (radius, 0, 0, 1), (0, 0, 0, 0)
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kLeafMaxPrims = 64;
 struct DeviceBvh {
-    std::vector<float> nodes;   // 16 floats per node
+    std::vector<float> nodes;   // 32 floats per 4-wide node
     std::vector<float> prims;   // 12 floats per primitive
     uint32_t num_nodes = 0;
-    uint32_t depth = 0;          // max inner-node depth (stack bound)
+    uint32_t depth = 0;          // max inner-node depth of the 4-wide tree (stack bound: 3 per level)
     uint32_t ref_nodes = 0;      // nodes of the reference-layout tree
     float sah_cost = 0;
 };

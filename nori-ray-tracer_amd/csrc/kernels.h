@@ -8,6 +8,7 @@ namespace nori {
 
 constexpr int kShadeBlock = 256;   // shade / regen work-group size
 constexpr int kTraceBlock = 128;   // traversal work-group size (LDS stack columns)
+constexpr int kTraceSpill = 64;    // traversal stack entries beyond the LDS part (private memory)
 #ifndef NORI_TRACE_GROUP
 #define NORI_TRACE_GROUP 4
 #endif

@@ -30,6 +30,16 @@ ND uint32_t rank_in(uint64_t mask) {  // set lanes of `mask` below this lane
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 // ------------------------------------------------------------------ traversal
+// Load through the global address space: the scene tables sit in a struct
+// of generic pointers, which would otherwise compile to FLAT loads (they also
+// count against lgkmcnt, which the LDS traversal stack waits on).  BVH
+// traversal always reads global memory (only scan-mode scenes are staged in LDS).
+typedef float gfloat4 __attribute__((ext_vector_type(4)));
+ND float4 gld(const float4 *p) {
+    const gfloat4 v = *(const __attribute__((address_space(1))) gfloat4 *)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 struct TRay {
     V3 o, d, rcp;
     float mint, maxt;
@@ -227,36 +237,76 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     ub = vb = 0.0f;
     r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
     if (r.maxt < r.mint) return false;
+    // 4-wide nodes: test the four child boxes, enter the nearest hit child and
+    // push the others farthest first.  Box tests are monotone (a child box lies
+    // inside its parent's and rounding keeps the slab test monotone), so the
+    // candidate primitives are exactly those of the reference's binary tree.
+    uint32_t spill[kTraceSpill];  // stack entries beyond the LDS part (rare)
+    auto push = [&](int &sp, uint32_t v) {
+        if (sp < STACK) stk[sp * kTraceBlock] = v;
+        else spill[sp - STACK] = v;
+        ++sp;
+    };
     uint32_t ref = 0;
     int sp = 0;
     bool found = false;
     for (;;) {
         if (!(ref & 0x80000000u)) {
-            const float4 *nd = S.nodes + 4 * (size_t)ref;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            float tl, tr;
-            bool hl = box_test(a, b, r, tl), hr = box_test(c, e, r, tr);
-            uint32_t lref = __float_as_uint(a.w), rref = __float_as_uint(b.w);
-            if (hl && hr) {
-                bool lf = tl <= tr;
-                stk[sp * kTraceBlock] = lf ? rref : lref;
-                ++sp;
-                ref = lf ? lref : rref;
-                continue;
-            }
-            if (hl || hr) {
-                ref = hl ? lref : rref;
+            const float4 *nd = S.nodes + 8 * (size_t)ref;
+            const float4 mnx = gld(nd), mny = gld(nd + 1), mnz = gld(nd + 2), mxx = gld(nd + 3), mxy = gld(nd + 4),
+                         mxz = gld(nd + 5), rf = gld(nd + 6);
+            float k0, k1, k2, k3;
+            bool h;
+            h = box_test(make_float4(mnx.x, mny.x, mnz.x, 0), make_float4(mxx.x, mxy.x, mxz.x, 0), r, k0);
+            k0 = h ? k0 : INF_F;
+            const bool h0 = h;
+            h = box_test(make_float4(mnx.y, mny.y, mnz.y, 0), make_float4(mxx.y, mxy.y, mxz.y, 0), r, k1);
+            k1 = h ? k1 : INF_F;
+            const bool h1 = h;
+            h = box_test(make_float4(mnx.z, mny.z, mnz.z, 0), make_float4(mxx.z, mxy.z, mxz.z, 0), r, k2);
+            k2 = h ? k2 : INF_F;
+            const bool h2 = h;
+            h = box_test(make_float4(mnx.w, mny.w, mnz.w, 0), make_float4(mxx.w, mxy.w, mxz.w, 0), r, k3);
+            k3 = h ? k3 : INF_F;
+            const bool h3 = h;
+            const int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+            if (nh > 0) {
+                // order (key, ref) by entry distance; misses (key inf, hit false) sort last
+                uint32_t c0 = __float_as_uint(rf.x), c1 = __float_as_uint(rf.y), c2 = __float_as_uint(rf.z),
+                         c3 = __float_as_uint(rf.w);
+                bool m0 = !h0, m1 = !h1, m2 = !h2, m3 = !h3;
+                auto cs = [](float &ka, uint32_t &ca, bool &ma, float &kb, uint32_t &cb, bool &mb) {
+                    const bool sw = ma > mb || (ma == mb && kb < ka);
+                    const float tk = ka;
+                    const uint32_t tc = ca;
+                    const bool tm = ma;
+                    ka = sw ? kb : ka;
+                    kb = sw ? tk : kb;
+                    ca = sw ? cb : ca;
+                    cb = sw ? tc : cb;
+                    ma = sw ? mb : ma;
+                    mb = sw ? tm : mb;
+                };
+                cs(k0, c0, m0, k1, c1, m1);
+                cs(k2, c2, m2, k3, c3, m3);
+                cs(k0, c0, m0, k2, c2, m2);
+                cs(k1, c1, m1, k3, c3, m3);
+                cs(k1, c1, m1, k2, c2, m2);
+                if (nh > 3) push(sp, c3);
+                if (nh > 2) push(sp, c2);
+                if (nh > 1) push(sp, c1);
+                ref = c0;
                 continue;
             }
         } else {
             uint32_t start = ref & 0x1FFFFFFu, end = start + ((ref >> 25) & 63u) + 1u;
             for (uint32_t i = start; i < end; ++i) {
                 const float4 *p = S.prims + 3 * (size_t)i;
-                float4 p0 = p[0], p1 = p[1];
+                float4 p0 = gld(p), p1 = gld(p + 1);
                 float t = 0, u = 0, v = 0;
                 bool h;
                 if (__float_as_uint(p1.w) == 0u) {
-                    float4 p2 = p[2];
+                    float4 p2 = gld(p + 2);
                     h = tri_hit(p0, p1, p2, r, t, u, v);
                 } else {
                     h = sphere_hit(p0, p1, r, t);
@@ -274,7 +324,7 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
         }
         if (sp == 0) break;
         --sp;
-        ref = stk[sp * kTraceBlock];
+        ref = sp < STACK ? stk[sp * kTraceBlock] : spill[sp - STACK];
     }
     (void)STACK;
     return found;
@@ -1163,7 +1213,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
     // tables; for small scenes they are staged into LDS first so the chain
     // runs at LDS latency instead of L2 latency.
     DevScene S = Sg;
-    if (Sg.blob_bytes) {
+    if (STACK == 0 && Sg.blob_bytes) {  // the BVH path reads global memory (gld)
         for (uint32_t i = threadIdx.x; i < Sg.blob_bytes / 16; i += kTraceBlock) blob_lds[i] = Sg.blob[i];
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
@@ -1426,11 +1476,11 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st) {
     dim3 g(2 * G), b(kTraceBlock);
     switch (stack) {
-    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;  // LDS-staged
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
     }
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,

@@ -375,11 +375,13 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     build_device_bvh(d, rmin, rmax, bvh);
     c.bvh_depth = bvh.depth;
     c.bvh_nodes = bvh.num_nodes;
-    if (bvh.depth <= 8) c.stack = 8;
-    else if (bvh.depth <= 16) c.stack = 16;
-    else if (bvh.depth <= 32) c.stack = 32;
-    else if (bvh.depth <= 64) c.stack = 64;
-    else throw NoriException(NORI_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+    // traversal stack: at most 3 entries per level of the 4-wide tree; the
+    // first `stack` live in LDS, up to kTraceSpill more in private memory
+    const uint32_t need = 3 * bvh.depth + 1;
+    if (need <= 8) c.stack = 8;
+    else if (need <= 16) c.stack = 16;
+    else c.stack = 32;
+    if (need > (uint32_t)c.stack + kTraceSpill) throw NoriException(NORI_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
     // Traversal strategy: scenes of at most kScanMaxPrims primitives are
     // intersected by a wave-uniform scan (scalar loads, no divergence), larger
     // ones by per-lane BVH traversal.  NORI_TRAVERSAL=bvh|scan overrides.
