@@ -63,6 +63,7 @@ struct DevScene {
     float invW, invH;
     float s2c[16];
     float c2w[16];
+    float cam_o[3];  // cameraToWorld * (0,0,0,1) / w (perspective.cpp:104)
     float near_clip, far_clip;
     float filter[NORI_FILTER_RESOLUTION + 1];
     float filter_radius, lookup;

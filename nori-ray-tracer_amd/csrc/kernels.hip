@@ -660,10 +660,7 @@ ND void camera_ray(const DevScene &S, float px, float py, V3 &o, V3 &d, float &m
     V3 dl = normalize(nearP);
     float invZ = 1.0f / dl.z;
     const float *c = S.c2w;
-    float w = ((c[12] * 0.0f + c[13] * 0.0f) + c[14] * 0.0f) + c[15];
-    o = V3{(((c[0] * 0.0f + c[1] * 0.0f) + c[2] * 0.0f) + c[3]) / w,
-           (((c[4] * 0.0f + c[5] * 0.0f) + c[6] * 0.0f) + c[7]) / w,
-           (((c[8] * 0.0f + c[9] * 0.0f) + c[10] * 0.0f) + c[11]) / w};
+    o = V3{S.cam_o[0], S.cam_o[1], S.cam_o[2]};  // cameraToWorld * (0,0,0,1), same for every ray (host)
     d = V3{(c[0] * dl.x + c[1] * dl.y) + c[2] * dl.z, (c[4] * dl.x + c[5] * dl.y) + c[6] * dl.z,
            (c[8] * dl.x + c[9] * dl.y) + c[10] * dl.z};
     mint = S.near_clip * invZ;
@@ -926,6 +923,12 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         float4 L = rec[ps.work];
         rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, L.w);
     }
+#ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
+    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
+        (void)next1D(ps.rng);
+        (void)next2D(ps.rng);
+    } else
+#endif
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
         const NeeSample ne = nee_sample(S, hs.p, ps.rng);
         BRec br;
@@ -951,7 +954,14 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     br.wi = to_local(hs.sh, -ps.d);
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
+#ifdef NORI_PROF_NO_SAMPLE  // profiling build only: a cheap reflection instead of BSDF sampling
+    V2 su = next2D(ps.rng);
+    br.wo = V3{su.x - 0.5f, su.y - 0.5f, 0.5f};
+    br.measure = kMeasureSolidAngle;
+    V3 w = V3{0.7f, 0.7f, 0.7f};
+#else
     V3 w = bsdf_sample(B, br, next2D(ps.rng));
+#endif
     if (is_zero(w)) return false;  // deviation D1: zero-weight samples end the path
     ps.beta = ps.beta * w;
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
@@ -982,6 +992,16 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, PathState 
     rec[w] = make_float4(0, 0, 0, 0);
 }
 
+// Closest hit of a path's ray (scan mode, TRACE builds of k_shade).
+ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
+    TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
+    float t, u, v;
+    uint32_t p;
+    uint32_t *no_stack = nullptr;
+    traverse<0, false>(S, r, no_stack, t, p, u, v);
+    *hit = make_float4(t, __uint_as_float(p), u, v);
+}
+
 #ifndef NORI_SHADE_WAVES
 #define NORI_SHADE_WAVES 6
 #endif
@@ -995,7 +1015,7 @@ template <int INTEG, bool TRACE>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
-    __shared__ uint32_t s_need[kShadeBlock / 64], s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64];
+    __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, q = b * kSeg + tid;
     const uint32_t n_in = seg.cnt[in_sel][b];
@@ -1015,29 +1035,20 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     so.emit = false;
     bool alive = false;
     if (tid < n_in) alive = shade_vertex<INTEG>(S, ps, hit, rec, so);
-    // ---- regenerate from this segment's work stream
-    const bool need = !alive;
-    const uint64_t mneed = __ballot(need), msh = __ballot(so.emit);
+    // ---- compaction: survivors first (in lane order), shadow rays likewise
+    const uint64_t mal = __ballot(alive), msh = __ballot(so.emit);
     if (lane_id() == 0) {
-        s_need[wave] = (uint32_t)__popcll(mneed);
+        s_al[wave] = (uint32_t)__popcll(mal);
         s_sh[wave] = (uint32_t)__popcll(msh);
     }
     const uint32_t cursor = seg.cursor[b];
     __syncthreads();
-    uint32_t need_off = rank_in(mneed), sh_off = rank_in(msh), need_tot = 0, sh_tot = 0;
+    uint32_t al_off = rank_in(mal), sh_off = rank_in(msh), al_tot = 0, sh_tot = 0;
     for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
-        need_off += w < wave ? s_need[w] : 0u;
+        al_off += w < wave ? s_al[w] : 0u;
         sh_off += w < wave ? s_sh[w] : 0u;
-        need_tot += s_need[w];
+        al_tot += s_al[w];
         sh_tot += s_sh[w];
-    }
-    bool fresh = false;
-    if (need) {
-        uint64_t w = stream_work(wd, b, cursor + need_off);
-        if (w < wd.total) {
-            regen_path(S, wd, (uint32_t)w, ps, rec);
-            alive = fresh = true;
-        }
     }
     if (so.emit) {
         uint32_t i = b * kSeg + sh_off;
@@ -1045,31 +1056,35 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         sq.ray_d[i] = make_float4(so.d.x, so.d.y, so.d.z, so.maxt);
         sq.payload[i] = make_float4(so.contrib.x, so.contrib.y, so.contrib.z, __uint_as_float(so.work));
     }
-    const uint64_t mal = __ballot(alive), mfresh = __ballot(fresh);
-    if (lane_id() == 0) s_al[wave] = (uint32_t)__popcll(mal) | ((uint32_t)__popcll(mfresh) << 16);
-    __syncthreads();
-    uint32_t al_off = rank_in(mal), al_tot = 0, fresh_tot = 0;
-    for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
-        al_off += w < wave ? (s_al[w] & 0xFFFFu) : 0u;
-        al_tot += s_al[w] & 0xFFFFu;
-        fresh_tot += s_al[w] >> 16;
-    }
-    if (TRACE) {
-        TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
-        if (!alive) r.maxt = -1.0f;  // lane takes part in the scan without a ray
-        float t, u, v;
-        uint32_t p;
-        uint32_t *no_stack = nullptr;
-        traverse<0, false>(Sg, r, no_stack, t, p, u, v);
-        if (alive) out.hit[b * kSeg + al_off] = make_float4(t, __uint_as_float(p), u, v);
-    }
+    if (TRACE && alive) trace_into(Sg, ps, out.hit + b * kSeg + al_off);
     if (alive) store_path(out, b * kSeg + al_off, ps);
+    // ---- regeneration: the free slots [al_tot, kSeg) take the next work ids of
+    // the segment's stream, so only the tail waves run the camera-ray code and
+    // a wave's new samples are adjacent pixels (stream_work increases with p)
+    const uint32_t need_tot = kSeg - al_tot;
+    if (tid >= al_tot) {
+        const uint64_t w = stream_work(wd, b, cursor + (tid - al_tot));
+        if (w < wd.total) {
+            PathState np;
+            regen_path(Sg, wd, (uint32_t)w, np, rec);
+            if (TRACE) trace_into(Sg, np, out.hit + q);
+            store_path(out, q, np);
+        }
+    }
     if (tid == 0) {
-        seg.cnt[in_sel ^ 1][b] = al_tot;
+        // new samples = the prefix of [cursor, cursor + need_tot) still inside the stream
+        uint32_t lo = 0, hi = need_tot;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (stream_work(wd, b, cursor + mid) < wd.total) lo = mid + 1;
+            else hi = mid;
+        }
+        const uint32_t fresh_tot = lo;
+        seg.cnt[in_sel ^ 1][b] = al_tot + fresh_tot;
         seg.shcnt[b] = sh_tot;
         seg.cursor[b] = cursor + need_tot;
         uint4 st = seg.stats[b];
-        seg.stats[b] = make_uint4(st.x + al_tot, st.y + sh_tot, st.z + fresh_tot, st.w);
+        seg.stats[b] = make_uint4(st.x + al_tot + fresh_tot, st.y + sh_tot, st.z + fresh_tot, st.w);
         if (stream_work(wd, b, cursor) < wd.total && stream_work(wd, b, cursor + need_tot) >= wd.total) {
             // the last segment to run dry tells the host (system-scope store to
             // host-mapped memory) -- no per-iteration readback is needed

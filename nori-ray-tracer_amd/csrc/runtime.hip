@@ -499,6 +499,13 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.invH = 1.0f / (float)cam.height;
     std::memcpy(S.s2c, cam.sample_to_camera, sizeof(S.s2c));
     std::memcpy(S.c2w, cam.camera_to_world, sizeof(S.c2w));
+    {  // perspective.cpp:104: Eigen's (c2w * (0,0,0,1)).hnormalized(), column order
+        const float *c = S.c2w;
+        const float w = ((c[12] * 0.0f + c[13] * 0.0f) + c[14] * 0.0f) + c[15];
+        S.cam_o[0] = (((c[0] * 0.0f + c[1] * 0.0f) + c[2] * 0.0f) + c[3]) / w;
+        S.cam_o[1] = (((c[4] * 0.0f + c[5] * 0.0f) + c[6] * 0.0f) + c[7]) / w;
+        S.cam_o[2] = (((c[8] * 0.0f + c[9] * 0.0f) + c[10] * 0.0f) + c[11]) / w;
+    }
     S.near_clip = cam.near_clip;
     S.far_clip = cam.far_clip;
     filter_table(cam, S.filter);
