@@ -117,7 +117,7 @@ def roofline(ts, samples):
     VALU issue rate (SQ_INSTS_VALU x 64 lanes per launch, rocprofv3) is given
     against the issue peak.
     """
-    launches = max(ts["iterations"], 1)
+    launches = max(ts["iterations"] * max(ts.get("stream_parts", 1), 1), 1)  # per kernel
     rc, rs = ts["rays_closest"], ts["rays_shadow"]
     kern = {
         "shade": ("k_shade", ts["ms_shade"], rc * (84 + 68) + rs * 48 + samples * 20),
@@ -244,6 +244,7 @@ def main():
                                 "shadow": ts["rays_shadow"] / samples_per_step,
                                 "finisher": ts["rays_finish"] / samples_per_step},
             "wavefront_iterations": ts["iterations"],
+            "stream_parts": ts.get("stream_parts", 1),
         }
         if world == 1 and not args.no_parity:
             out["parity"] = parity_check()

@@ -212,9 +212,12 @@ typedef struct nori_gpu_stats {
     uint64_t rays_closest;        /* extension rays traced by k_extend          */
     uint64_t rays_shadow;         /* shadow rays traced by k_shadow             */
     uint64_t rays_finish;         /* rays traced inside the tail finisher       */
-    uint64_t iterations;          /* wavefront iterations (= extend launches)   */
+    uint64_t iterations;          /* wavefront iterations                       */
     uint64_t scene_bytes;         /* BVH nodes + primitive records in HBM       */
     uint32_t bvh_nodes, bvh_depth;
+    uint32_t stream_parts;        /* pool parts on their own streams: each kernel
+                                     runs stream_parts launches per iteration  */
+    uint32_t reserved;
     double ms_total;              /* render wall time (host timer)              */
     /* with desc.timing: summed HIP-event time of each kernel, on the launch stream */
     double ms_extend, ms_shadow, ms_shade, ms_splat, ms_finish;

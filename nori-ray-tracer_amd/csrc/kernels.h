@@ -39,7 +39,7 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 // launch_extend is then skipped).
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                        hipStream_t st);
+                        uint32_t nseg, hipStream_t st);
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,

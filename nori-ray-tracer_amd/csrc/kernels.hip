@@ -1063,7 +1063,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     // a wave's new samples are adjacent pixels (stream_work increases with p)
     const uint32_t need_tot = kSeg - al_tot;
     if (tid >= al_tot) {
-        const uint64_t w = stream_work(wd, b, cursor + (tid - al_tot));
+        const uint64_t w = stream_work(wd, wd.b0 + b, cursor + (tid - al_tot));
         if (w < wd.total) {
             PathState np;
             regen_path(Sg, wd, (uint32_t)w, np, rec);
@@ -1076,7 +1076,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         uint32_t lo = 0, hi = need_tot;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (stream_work(wd, b, cursor + mid) < wd.total) lo = mid + 1;
+            if (stream_work(wd, wd.b0 + b, cursor + mid) < wd.total) lo = mid + 1;
             else hi = mid;
         }
         const uint32_t fresh_tot = lo;
@@ -1085,7 +1085,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         seg.cursor[b] = cursor + need_tot;
         uint4 st = seg.stats[b];
         seg.stats[b] = make_uint4(st.x + al_tot + fresh_tot, st.y + sh_tot, st.z + fresh_tot, st.w);
-        if (stream_work(wd, b, cursor) < wd.total && stream_work(wd, b, cursor + need_tot) >= wd.total) {
+        if (stream_work(wd, wd.b0 + b, cursor) < wd.total && stream_work(wd, wd.b0 + b, cursor + need_tot) >= wd.total) {
             // the last segment to run dry tells the host (system-scope store to
             // host-mapped memory) -- no per-iteration readback is needed
             uint32_t n = atomicAdd(&C->exhausted, 1u) + 1u;
@@ -1422,8 +1422,8 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 template <int INTEG>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                           uint32_t lds, hipStream_t st) {
-    dim3 g(wd.G), b(kShadeBlock);
+                           uint32_t lds, uint32_t nseg, hipStream_t st) {
+    dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
     if (trace)
         hipLaunchKernelGGL((k_shade<INTEG, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
@@ -1431,16 +1431,17 @@ static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQue
 }
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                        hipStream_t st) {
+                        uint32_t nseg, hipStream_t st) {
+    if (nseg == 0 || wd.b0 + nseg > wd.G) return hipErrorInvalidValue;
     const uint32_t lds = S.blob_bytes <= kShadeLdsMax ? S.blob_bytes : 0u;
     switch (S.integrator) {
     case NORI_INTEGRATOR_PATH_MATS:
-        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, st);
+        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
         break;
     case NORI_INTEGRATOR_VOLUMETRIC:
-        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, st);
+        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
         break;
-    default: shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, st); break;
+    default: shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st); break;
     }
     return hipGetLastError();
 }

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -179,11 +180,15 @@ struct nori_scene {
     std::unique_ptr<HostScene> hs;
 };
 
+constexpr int kMaxParts = 4;  // pool parts on separate streams (GPU_MAX_HW_QUEUES is 4)
+
 struct nori_gpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;       // film splat, overlapped with the tail finisher
     hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t parts[kMaxParts] = {};  // parts[0] unused (part 0 runs on `stream`)
+    hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob;
@@ -197,9 +202,14 @@ struct nori_gpu_ctx {
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
     uint32_t *pinned_dev = nullptr;  // device view of `pinned`
-    std::vector<hipEvent_t> ring;
+    std::vector<hipEvent_t> ring[kMaxParts];
     ~nori_gpu_ctx() {
-        for (auto e : ring) (void)hipEventDestroy(e);
+        for (auto &r : ring)
+            for (auto e : r) (void)hipEventDestroy(e);
+        for (int h = 1; h < kMaxParts; ++h) {
+            if (joins[h]) (void)hipEventDestroy(joins[h]);
+            if (parts[h]) (void)hipStreamDestroy(parts[h]);
+        }
         if (pinned) (void)hipHostFree(pinned);
         if (fork) (void)hipEventDestroy(fork);
         if (join) (void)hipEventDestroy(join);
@@ -576,6 +586,11 @@ bool debug_log() {
     const char *e = std::getenv("NORI_DEBUG");
     return e && e[0] == '1';
 }
+uint32_t pool_parts() {  // NORI_POOL_PARTS: independent pool parts on their own streams (1..kMaxParts)
+    const char *e = std::getenv("NORI_POOL_PARTS");
+    const long v = e ? std::atol(e) : 2;
+    return (uint32_t)(v >= 1 && v <= kMaxParts ? v : 2);
+}
 uint64_t event_every() {  // NORI_EVENT_EVERY: iterations per host event (default 1)
     const char *e = std::getenv("NORI_EVENT_EVERY");
     const long v = e ? std::atol(e) : 1;
@@ -648,8 +663,10 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         // host-mapped, coherent: the shade kernel stores the completion flag here
         HIP_TRY(hipHostMalloc((void **)&c.pinned, 256, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void **)&c.pinned_dev, c.pinned, 0));
-        c.ring.resize(kRing);
-        for (auto &e : c.ring) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto &r : c.ring) {
+            r.resize(kRing);
+            for (auto &e : r) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
     }
     Counters *C = c.counters.as<Counters>();
     ShadowQueue sq{c.sq[0].as<float4>(), c.sq[1].as<float4>(), c.sq[2].as<float4>()};
@@ -682,6 +699,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // the shade kernel (measured even with separate k_extend launches)
     const bool fused = c.stack == 0 && fused_extend();
     const uint64_t every = event_every();
+    const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(), pool / kSeg));
     const uint32_t G = pool / kSeg;
     SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
                  c.segstats.as<uint4>()};
@@ -689,7 +707,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     uint64_t finish_rays = 0, samples_started = 0;
     for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
         uint32_t np = std::min(chunk, passes - p0);
-        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev, 1};
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev, 1, 0};
         wd.rot = stream_rotation(wd.total, M, G);
         __atomic_store_n(&c.pinned[0], 0u, __ATOMIC_RELEASE);
         __atomic_store_n(&c.pinned[1], 0u, __ATOMIC_RELEASE);
@@ -702,24 +720,59 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipMemsetAsync(seg.cursor, 0, 4 * (size_t)G, c.stream));
         HIP_TRY(hipMemsetAsync(seg.stats, 0, 16 * (size_t)G, c.stream));
         int last_out = 0;
+        // The pool is split into `parts` independent parts (segments never
+        // interact), each driven on its own stream: the memory-bound shade
+        // launch of one part overlaps the VALU-bound traversal of another.
+        std::vector<uint32_t> Gp(parts), base(parts);
+        for (uint32_t h = 0; h < parts; ++h) {
+            base[h] = (uint32_t)((uint64_t)G * h / parts);
+            Gp[h] = (uint32_t)((uint64_t)G * (h + 1) / parts) - base[h];
+        }
+        auto q_view = [&](const PathQueue &q, uint32_t b0) {
+            const size_t e = (size_t)b0 * kSeg;
+            return PathQueue{q.ray_o + e, q.ray_d + e, q.hit + e, q.thr + e, q.rng + e, q.work + e};
+        };
+        std::vector<std::array<PathQueue, 2>> Qh(parts);
+        std::vector<ShadowQueue> sqh(parts);
+        std::vector<SegState> segh(parts);
+        std::vector<WorkDesc> wdh(parts);
+        for (uint32_t h = 0; h < parts; ++h) {
+            Qh[h][0] = q_view(Q[0], base[h]);
+            Qh[h][1] = q_view(Q[1], base[h]);
+            const size_t e = (size_t)base[h] * kSeg;
+            sqh[h] = ShadowQueue{sq.ray_o + e, sq.ray_d + e, sq.payload + e};
+            segh[h] = SegState{{seg.cnt[0] + base[h], seg.cnt[1] + base[h]}, seg.shcnt + base[h],
+                               seg.cursor + base[h], seg.stats + base[h]};
+            wdh[h] = wd;
+            wdh[h].b0 = base[h];
+        }
+        HIP_TRY(hipEventRecord(c.fork, c.stream));  // the part streams start after the resets above
+        for (uint32_t h = 1; h < parts; ++h) HIP_TRY(hipStreamWaitEvent(c.parts[h], c.fork, 0));
         for (uint64_t it = 0;; ++it) {
             int in = (int)(it & 1), out = in ^ 1;
             last_out = out;
-            timed(2, [&] {
-                return launch_shade(S, Q[in], Q[out], sq, seg, in, wd, c.rec.as<float4>(), C, fused, c.stream);
-            });
-            if (!fused) timed(0, [&] { return launch_extend(S, Q[out], seg.cnt[out], G, c.stack, c.stream); });
-            timed(1, [&] { return launch_shadow(S, sq, seg.shcnt, c.rec.as<float4>(), G, c.stack, c.stream); });
+            for (uint32_t h = 0; h < parts; ++h) {
+                hipStream_t st = h ? c.parts[h] : c.stream;
+                const SegState &sg = segh[h];
+                timed_on(st, 2, [&] {
+                    return launch_shade(S, Qh[h][in], Qh[h][out], sqh[h], sg, in, wdh[h], c.rec.as<float4>(), C,
+                                        fused, Gp[h], st);
+                });
+                if (!fused)
+                    timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st); });
+                timed_on(st, 1, [&] { return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st); });
+            }
             ++iters;
             // an event every `every` iterations (each record adds a gap
             // between dependent kernels); the host waits on the one from at
             // least kLookahead iterations back
             if ((it + 1) % every != 0) continue;
             const uint64_t ev = it / every;
-            HIP_TRY(hipEventRecord(c.ring[ev % kRing], c.stream));
+            for (uint32_t h = 0; h < parts; ++h)
+                HIP_TRY(hipEventRecord(c.ring[h][ev % kRing], h ? c.parts[h] : c.stream));
             const uint64_t lag = (kLookahead + every - 1) / every;
             if (ev >= lag) {
-                HIP_TRY(hipEventSynchronize(c.ring[(ev - lag) % kRing]));
+                for (uint32_t h = 0; h < parts; ++h) HIP_TRY(hipEventSynchronize(c.ring[h][(ev - lag) % kRing]));
                 uint32_t exhausted = __atomic_load_n(&c.pinned[1], __ATOMIC_ACQUIRE);
                 c.progress = (float)std::min(1.0, (double)done_before / (double)total_all +
                                                       (double)np / passes * exhausted / G);
@@ -730,6 +783,10 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                     break;
                 }
             }
+        }
+        for (uint32_t h = 1; h < parts; ++h) {  // join: the tail below runs on the whole pool
+            HIP_TRY(hipEventRecord(c.joins[h], c.parts[h]));
+            HIP_TRY(hipStreamWaitEvent(c.stream, c.joins[h], 0));
         }
         if (cancelled) break;
         // The samples still in flight are marked pending; the film splat of all
@@ -783,6 +840,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         for (size_t i = 0; i < film_elems; ++i) rgbw_out[i] += hf[i];
     }
     HIP_TRY(hipStreamSynchronize(c.stream));
+    HIP_TRY(hipStreamSynchronize(c.side));
+    for (int h = 1; h < kMaxParts; ++h) HIP_TRY(hipStreamSynchronize(c.parts[h]));
     c.progress = 1.0f;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -794,6 +853,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         stats->scene_bytes = c.scene_bytes;
         stats->bvh_nodes = c.bvh_nodes;
         stats->bvh_depth = c.bvh_depth;
+        stats->stream_parts = parts;
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->ms_extend = kms[0];
         stats->ms_shadow = kms[1];
@@ -891,6 +951,10 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         c->device = device;
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        for (int h = 1; h < kMaxParts; ++h) {
+            HIP_TRY(hipStreamCreateWithFlags(&c->parts[h], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&c->joins[h], hipEventDisableTiming));
+        }
         HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         upload_scene(*c, *d);
