@@ -47,8 +47,10 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
 // Marks the record of every queued path pending (w = 1): k_splat skips it.
 hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st);
 // Completes every queued path and splats its sample into `film` itself.
+// (pre: G + 1 words of scratch for the prefix over the segment counts)
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
-                         const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st);
+                         const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
+                         hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 

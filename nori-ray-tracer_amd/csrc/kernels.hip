@@ -1216,14 +1216,39 @@ constexpr int kCoopMax = 4;
 // Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
 // bounce) would otherwise cost three launches per bounce.  Waves loop while
 // any lane's path is alive so that the lanes can trace cooperatively.
+// Exclusive prefix of the queued-path counts of the G segments (pre[G] = total).
+__global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint32_t G, uint32_t *pre) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, per = (G + 1023) / 1024, b = t * per, e = min(G, b + per);
+    uint32_t sum = 0;
+    for (uint32_t i = b; i < e; ++i) sum += cnt[i];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = t ? part[t - 1] : 0u;
+    for (uint32_t i = b; i < e; ++i) {
+        pre[i] = run;
+        run += cnt[i];
+    }
+    if (t == 1023) pre[G] = part[1023];
+}
+
 template <int STACK, int INTEG>
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
-                                                        float4 *rec, WorkDesc wd, float *film, Counters *C) {
+                                                        float4 *rec, WorkDesc wd, float *film, Counters *C,
+                                                        const uint32_t *pre, uint32_t G) {
     __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
-    const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
-    const uint32_t n = seg.cnt[sel][sg];
-    if ((blockIdx.x & 1) * kTraceBlock >= n) return;  // whole block idle
+    // the queued paths of all segments, numbered through the prefix `pre`
+    // (k_tail_prefix) so that they fill whole waves: few waves, each with a
+    // SIMD to itself, instead of one or two lanes in thousands of waves
+    const uint32_t n = pre[G], gid = blockIdx.x * kTraceBlock + threadIdx.x;
+    if (blockIdx.x * kTraceBlock >= n) return;  // whole block idle
     // Each bounce of a tail path is a chain of dependent reads of small
     // tables; for small scenes they are staged into LDS first so the chain
     // runs at LDS latency instead of L2 latency.
@@ -1233,9 +1258,19 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
     }
-    if ((idx & ~63u) >= n) return;  // whole wave idle
-    const uint32_t q = sg * kSeg + idx;
-    bool active = idx < n;
+    if ((gid & ~63u) >= n) return;  // whole wave idle
+    bool active = gid < n;
+    uint32_t sg = 0;
+    if (active) {  // segment of path gid: last s with pre[s] <= gid
+        uint32_t lo = 0, hi = G;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= gid) lo = mid;
+            else hi = mid;
+        }
+        sg = lo;
+    }
+    const uint32_t q = sg * kSeg + (active ? gid - pre[sg] : 0u);
     PathState ps;
     float4 h = make_float4(0, 0, 0, 0);
     if (active) {
@@ -1489,24 +1524,27 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 
 template <int INTEG>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
-                            const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st) {
-    dim3 g(2 * G), b(kTraceBlock);
+                            const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_tail_prefix, dim3(1), dim3(1024), 0, st, seg.cnt[sel], G, pre);
+    dim3 g(2 * G), b(kTraceBlock);  // enough blocks for a full pool; the idle ones exit at once
     switch (stack) {
-    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C); break;  // LDS-staged
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C); break;
+    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;  // LDS-staged
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
-                         const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, hipStream_t st) {
+                         const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
+                         hipStream_t st) {
     if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
+        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else if (S.integrator == NORI_INTEGRATOR_VOLUMETRIC)
-        finish_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
+        finish_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else
-        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, st);
+        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     return hipGetLastError();
 }
 

@@ -198,7 +198,7 @@ struct nori_gpu_ctx {
     std::atomic<int> cancel{0};
     std::atomic<float> progress{1.0f};
     // render state
-    DevBuf q[2][6], sq[3], seg[4], segstats, rec, counters, pixels, blocks, film;
+    DevBuf q[2][6], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
     uint32_t *pinned_dev = nullptr;  // device view of `pinned`
@@ -549,6 +549,7 @@ void ensure_pool(nori_gpu_ctx &c, uint32_t pool) {
     for (int k = 0; k < 3; ++k) c.sq[k].ensure(16 * (size_t)pool);
     for (int k = 0; k < 4; ++k) c.seg[k].ensure(4 * (size_t)(pool / kSeg));
     c.segstats.ensure(16 * (size_t)(pool / kSeg));
+    c.tailpre.ensure(4 * (size_t)(pool / kSeg + 1));
     c.pool_cap = pool;
 }
 
@@ -700,6 +701,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     const bool fused = c.stack == 0 && fused_extend();
     const uint64_t every = event_every();
     const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(), pool / kSeg));
+    const char *stg = std::getenv("NORI_PART_STAGGER");
+    const bool stagger = stg && stg[0] == '1';
     const uint32_t G = pool / kSeg;
     SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
                  c.segstats.as<uint4>()};
@@ -758,6 +761,11 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                     return launch_shade(S, Qh[h][in], Qh[h][out], sqh[h], sg, in, wdh[h], c.rec.as<float4>(), C,
                                         fused, Gp[h], st);
                 });
+                if (it == 0 && h == 0 && parts > 1 && stagger) {
+                    // NORI_PART_STAGGER=1: the other parts start after part 0's first shade
+                    HIP_TRY(hipEventRecord(c.fork, c.stream));
+                    for (uint32_t k = 1; k < parts; ++k) HIP_TRY(hipStreamWaitEvent(c.parts[k], c.fork, 0));
+                }
                 if (!fused)
                     timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st); });
                 timed_on(st, 1, [&] { return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st); });
@@ -802,7 +810,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                      c.blocks.as<int4>(), rd.seed};
         timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
         timed(4, [&] {
-            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack, c.stream);
+            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack, c.tailpre.as<uint32_t>(), c.stream);
         });
         HIP_TRY(hipEventRecord(c.join, c.side));
         HIP_TRY(hipStreamWaitEvent(c.stream, c.join, 0));
