@@ -800,6 +800,31 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
     return r;
 }
 
+#ifndef NORI_SHADE_ATOMIC_REC
+#define NORI_SHADE_ATOMIC_REC 1
+#endif
+// Emission found by the shade kernel, added to the sample record.  Each record
+// has one path, and the shadow kernel's read-modify-write of it runs in a later
+// launch, so the adds need no atomicity -- but returnless atomics do not make
+// the wave wait for the record's read (a full memory latency in most waves);
+// IEEE adds in the same order, so the sums are identical.
+// ATOMIC false: the caller reads the record back in the same kernel (finisher),
+// where a plain load could hit an L1 line the L2-side atomic left stale.
+template <bool ATOMIC>
+ND void rec_add(float4 *rec, uint32_t w, const V3 &a) {
+#if NORI_SHADE_ATOMIC_REC
+    if (ATOMIC) {
+        float *r = reinterpret_cast<float *>(rec + w);
+        atomicAdd(r + 0, a.x);
+        atomicAdd(r + 1, a.y);
+        atomicAdd(r + 2, a.z);
+        return;
+    }
+#endif
+    const float4 L = rec[w];
+    rec[w] = make_float4(L.x + a.x, L.y + a.y, L.z + a.z, L.w);
+}
+
 // One iteration of VolumetricIntegrator::Li (volumetric.cpp:18-156) for the
 // current segment (ps.o, ps.d) and its closest hit h (prim ~0: none, t = inf).
 // Free flight first: a scattering event does phase-function NEE with
@@ -807,6 +832,7 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
 // the surface vertex does path_mis-style emission and NEE, both weighted by
 // transmittance.  ps.prev carries the pdf for w_mats at the next emitter hit
 // (1/4pi after a scattering event, -1 after a discrete lobe).
+template <bool ATOMIC>
 ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
     so.emit = false;
     const uint32_t prim = __float_as_uint(h.y);
@@ -853,8 +879,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
             w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
         }
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
-        float4 L = rec[ps.work];
-        rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, L.w);
+        rec_add<ATOMIC>(rec, ps.work, Ladd);
     }
     {
         NeeSample ne = nee_sample(S, hs.p, ps.rng);
@@ -896,9 +921,9 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
 // One vertex of PathMisIntegrator::Li (path_mis.cpp:32-97) or
 // PathMatsIntegrator::Li (path_mats.cpp:26-57) given the closest hit of the
 // current ray.  Returns true if the path continues (ps holds the new ray).
-template <int INTEG>
+template <int INTEG, bool ATOMIC>
 ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
-    if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol(S, ps, h, rec, so);
+    if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol<ATOMIC>(S, ps, h, rec, so);
     so.emit = false;
     uint32_t prim = __float_as_uint(h.y);
     if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
@@ -920,8 +945,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         } else {
             Ladd = ps.beta * Le;
         }
-        float4 L = rec[ps.work];
-        rec[ps.work] = make_float4(L.x + Ladd.x, L.y + Ladd.y, L.z + Ladd.z, L.w);
+        rec_add<ATOMIC>(rec, ps.work, Ladd);
     }
 #ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
@@ -1003,7 +1027,7 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
 }
 
 #ifndef NORI_SHADE_WAVES
-#define NORI_SHADE_WAVES 6
+#define NORI_SHADE_WAVES 5
 #endif
 // lds_bytes != 0: the scene blob is staged into LDS first, so the chains of
 // dependent table reads of a vertex (shape -> bsdf -> vertices -> light CDF)
@@ -1034,7 +1058,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     ShadowOut so;
     so.emit = false;
     bool alive = false;
-    if (tid < n_in) alive = shade_vertex<INTEG>(S, ps, hit, rec, so);
+    if (tid < n_in) alive = shade_vertex<INTEG, true>(S, ps, hit, rec, so);
     // ---- compaction: survivors first (in lane order), shadow rays likewise
     const uint64_t mal = __ballot(alive), msh = __ballot(so.emit);
     if (lane_id() == 0) {
@@ -1238,6 +1262,9 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
     if (t == 1023) pre[G] = part[1023];
 }
 
+#ifndef NORI_FINISH_PRIO
+#define NORI_FINISH_PRIO 1
+#endif
 template <int STACK, int INTEG>
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
@@ -1259,6 +1286,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
     }
     if ((gid & ~63u) >= n) return;  // whole wave idle
+#if NORI_FINISH_PRIO
+    // the film splat runs beside the finisher: its waves must not take the
+    // issue slots of these few latency-bound ones
+    __builtin_amdgcn_s_setprio(3);
+#endif
     bool active = gid < n;
     uint32_t sg = 0;
     if (active) {  // segment of path gid: last s with pre[s] <= gid
@@ -1289,7 +1321,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         ShadowOut so;
         so.emit = false;
         bool alive = false;
-        if (active) alive = shade_vertex<INTEG>(S, ps, h, rec, so);
+        if (active) alive = shade_vertex<INTEG, false>(S, ps, h, rec, so);
         {
             TRay r{so.o, so.d, V3{0, 0, 0}, kEps, so.maxt};
             float t, u, v;

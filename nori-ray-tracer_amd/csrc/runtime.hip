@@ -640,7 +640,11 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
     // default pool: 4M paths in flight (~0.9 GB of queues); measured best among
     // 256K..4M on cbox (larger pools hide the shade kernel's memory latency)
-    uint32_t pool = rd.path_pool ? rd.path_pool : (1u << 22);
+    uint32_t pool = rd.path_pool;
+    if (!pool) {  // NORI_PATH_POOL: default pool size override (tuning)
+        const char *e = std::getenv("NORI_PATH_POOL");
+        pool = e && std::atol(e) > 0 ? (uint32_t)std::min<long>(std::atol(e), 1L << 26) : (1u << 22);
+    }
     pool = std::max<uint32_t>(kSeg, (pool + kSeg - 1) / kSeg * kSeg);
     ensure_pool(c, pool);
     // sample-record budget: chunks of passes, each < 2^31 records

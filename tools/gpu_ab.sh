@@ -13,6 +13,7 @@ for r in $(seq 1 $reps); do
     rc=$?; if [ $rc -ne 0 ]; then echo "$c rc=$rc"; tail -3 gpurun_out/ab.log; exit $rc; fi
     v=$(grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; print(round(json.loads(sys.stdin.read())['value'],1))")
     echo "$c $v" | tee -a gpurun_out/ab_results.txt
+    grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; k=json.loads(sys.stdin.read()).get('kernel_ms',{}); print('   kernel_ms', {a: round(b,2) for a,b in k.items()})"
   done
 done
 python3 - <<'PY'
