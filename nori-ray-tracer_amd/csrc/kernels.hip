@@ -1042,13 +1042,16 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, q = b * kSeg + tid;
+    // every load the work-group needs is issued up front, so their latencies
+    // overlap instead of adding up: the segment's bookkeeping (scalar), and
+    // the path entries whether or not they hold a path (a queue slot beyond
+    // the count is stale but allocated; nothing reads its values)
     const uint32_t n_in = seg.cnt[in_sel][b];
+    const uint32_t cursor = seg.cursor[b];
+    const uint4 st0 = seg.stats[b];
     PathState ps;
-    float4 hit;
-    if (tid < n_in) {  // path loads in flight while the blob is staged
-        load_path(in, q, ps);
-        hit = in.hit[q];
-    }
+    load_path(in, q, ps);
+    const float4 hit = in.hit[q];
     DevScene S = Sg;
     if (lds_bytes) {
         for (uint32_t i = tid; i < lds_bytes / 16; i += kShadeBlock) blob_lds[i] = Sg.blob[i];
@@ -1065,7 +1068,6 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         s_al[wave] = (uint32_t)__popcll(mal);
         s_sh[wave] = (uint32_t)__popcll(msh);
     }
-    const uint32_t cursor = seg.cursor[b];
     __syncthreads();
     uint32_t al_off = rank_in(mal), sh_off = rank_in(msh), al_tot = 0, sh_tot = 0;
     for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
@@ -1107,8 +1109,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         seg.cnt[in_sel ^ 1][b] = al_tot + fresh_tot;
         seg.shcnt[b] = sh_tot;
         seg.cursor[b] = cursor + need_tot;
-        uint4 st = seg.stats[b];
-        seg.stats[b] = make_uint4(st.x + al_tot + fresh_tot, st.y + sh_tot, st.z + fresh_tot, st.w);
+        seg.stats[b] = make_uint4(st0.x + al_tot + fresh_tot, st0.y + sh_tot, st0.z + fresh_tot, st0.w);
         if (stream_work(wd, wd.b0 + b, cursor) < wd.total && stream_work(wd, wd.b0 + b, cursor + need_tot) >= wd.total) {
             // the last segment to run dry tells the host (system-scope store to
             // host-mapped memory) -- no per-iteration readback is needed
