@@ -162,7 +162,8 @@ struct Counters {
     uint32_t exhausted;            // segments whose work stream is used up
     uint32_t pad0[31];
     unsigned long long invalid;    // dropped samples (splat)
-    unsigned long long pad1[15];
+    unsigned long long prof[8];    // profiling builds only (NORI_PROF_FINISH): finisher phase clocks
+    unsigned long long pad1[7];
     uint32_t finish_paths;         // paths completed by the tail finisher
     uint32_t finish_max_rays;      // most rays traced by one finisher path
     uint32_t pad2[30];

@@ -360,9 +360,9 @@ struct SegRange {
     uint32_t s0;
 };
 constexpr uint32_t kTraceSlices = kTraceGroup * kSeg / kTraceBlock;  // work-groups per group
-ND SegRange seg_range(const uint32_t *cnt, uint32_t G) {
+ND SegRange seg_range(const uint32_t *cnt, uint32_t G, uint32_t bid) {
     SegRange r;
-    r.s0 = (blockIdx.x / kTraceSlices) * kTraceGroup;
+    r.s0 = (bid / kTraceSlices) * kTraceGroup;
     r.pre[0] = 0;
 #pragma unroll
     for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
@@ -386,12 +386,13 @@ ND uint32_t seg_entry(const SegRange &r, uint32_t i) {
     return (r.s0 + k) * kSeg + (i - base);
 }
 
-// Extension rays: closest hit of every queued path.
+// Extension rays: closest hit of every queued path (work-group `bid` of the
+// launch's extension part).
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
-    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
-    const SegRange sr = seg_range(cnt, G);
-    const uint32_t i = (blockIdx.x % kTraceSlices) * kTraceBlock + threadIdx.x;
+ND void extend_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt, uint32_t G, uint32_t bid,
+                    uint32_t *stk) {
+    const SegRange sr = seg_range(cnt, G, bid);
+    const uint32_t i = (bid % kTraceSlices) * kTraceBlock + threadIdx.x;
     if (i < sr.pre[kTraceGroup]) {
         const uint32_t q = seg_entry(sr, i);
         float4 a = pq.ray_o[q], b = pq.ray_d[q];
@@ -409,11 +410,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq
 
 // Shadow rays: any hit; unoccluded -> record += payload.
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
-                                                        float4 *rec, uint32_t G) {
-    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
-    const SegRange sr = seg_range(shcnt, G);
-    const uint32_t i = (blockIdx.x % kTraceSlices) * kTraceBlock + threadIdx.x;
+ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
+                    uint32_t bid, uint32_t *stk) {
+    const SegRange sr = seg_range(shcnt, G, bid);
+    const uint32_t i = (bid % kTraceSlices) * kTraceBlock + threadIdx.x;
     if (i < sr.pre[kTraceGroup]) {
         const uint32_t q = seg_entry(sr, i);
         float4 a = sq.ray_o[q], b = sq.ray_d[q];
@@ -433,6 +433,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue 
     }
 }
 
+template <int STACK>
+__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
+    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    extend_body<STACK>(S, pq, cnt, G, blockIdx.x, stk);
+}
+template <int STACK>
+__global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
+                                                        float4 *rec, uint32_t G) {
+    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    shadow_body<STACK>(S, sq, shcnt, rec, G, blockIdx.x, stk);
+}
 // Scan-mode traversal of K rays per thread: every primitive record is
 // fetched once (scalar loads) and tested against K independent rays, which
 // gives the VALU K independent dependency chains to interleave.  Results are
@@ -675,6 +686,7 @@ struct PathState {
     float prev;  // BSDF pdf of the last bounce; -1: w_mats = 1 (camera ray or discrete lobe)
     Pcg rng;
     uint32_t work;
+    V3 L;  // finisher only: the sample's radiance so far (the record, held in registers)
 };
 struct ShadowOut {
     bool emit;
@@ -808,21 +820,24 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
 // launch, so the adds need no atomicity -- but returnless atomics do not make
 // the wave wait for the record's read (a full memory latency in most waves);
 // IEEE adds in the same order, so the sums are identical.
-// ATOMIC false: the caller reads the record back in the same kernel (finisher),
-// where a plain load could hit an L1 line the L2-side atomic left stale.
+// ATOMIC false (finisher): the sum is kept in ps.L, in registers -- a tail
+// path's bounces are a serial chain, and a record read per bounce would add a
+// memory latency to each.
 template <bool ATOMIC>
-ND void rec_add(float4 *rec, uint32_t w, const V3 &a) {
-#if NORI_SHADE_ATOMIC_REC
-    if (ATOMIC) {
-        float *r = reinterpret_cast<float *>(rec + w);
-        atomicAdd(r + 0, a.x);
-        atomicAdd(r + 1, a.y);
-        atomicAdd(r + 2, a.z);
+ND void rec_add(float4 *rec, PathState &ps, const V3 &a) {
+    if (!ATOMIC) {
+        ps.L = ps.L + a;
         return;
     }
+#if NORI_SHADE_ATOMIC_REC
+    float *r = reinterpret_cast<float *>(rec + ps.work);
+    atomicAdd(r + 0, a.x);
+    atomicAdd(r + 1, a.y);
+    atomicAdd(r + 2, a.z);
+#else
+    const float4 L = rec[ps.work];
+    rec[ps.work] = make_float4(L.x + a.x, L.y + a.y, L.z + a.z, L.w);
 #endif
-    const float4 L = rec[w];
-    rec[w] = make_float4(L.x + a.x, L.y + a.y, L.z + a.z, L.w);
 }
 
 // One iteration of VolumetricIntegrator::Li (volumetric.cpp:18-156) for the
@@ -879,7 +894,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
             w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
         }
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
-        rec_add<ATOMIC>(rec, ps.work, Ladd);
+        rec_add<ATOMIC>(rec, ps, Ladd);
     }
     {
         NeeSample ne = nee_sample(S, hs.p, ps.rng);
@@ -945,7 +960,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         } else {
             Ladd = ps.beta * Le;
         }
-        rec_add<ATOMIC>(rec, ps.work, Ladd);
+        rec_add<ATOMIC>(rec, ps, Ladd);
     }
 #ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
@@ -1000,9 +1015,10 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
 }
 
 // New camera sample for work id w (render.cpp:98-126 + independent.cpp).
-ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, PathState &ps, float4 *rec) {
-    uint32_t pass = w / wd.M, e = w - pass * wd.M;
-    uint32_t pix = wd.pixels[e];
+// pix = wd.pixels[w mod M], loaded by the caller (early: a load issued
+// after the path stores would wait for them too -- vmcnt counts in order)
+ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t pix, PathState &ps, float4 *rec) {
+    uint32_t pass = w / wd.M;
     uint32_t W = (uint32_t)S.W;
     uint32_t y = pix / W, x = pix - y * W;
     uint64_t sid = (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix;
@@ -1039,9 +1055,21 @@ template <int INTEG, bool TRACE>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
-    __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64];
+    static_assert(kShadeBlock == kSeg, "one shade thread per segment slot");
+    __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64], s_w[kSeg], s_pix[kSeg];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, q = b * kSeg + tid;
+#ifdef NORI_PROF_SHADE  // profiling build: clocks of the kernel's phases, summed over waves
+    uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, pc = __builtin_amdgcn_s_memtime();
+#define NORI_SPHASE(i)                                       \
+    {                                                        \
+        const uint64_t now = __builtin_amdgcn_s_memtime();   \
+        pt[i] += now - pc;                                   \
+        pc = now;                                            \
+    }
+#else
+#define NORI_SPHASE(i)
+#endif
     // every load the work-group needs is issued up front, so their latencies
     // overlap instead of adding up: the segment's bookkeeping (scalar), and
     // the path entries whether or not they hold a path (a queue slot beyond
@@ -1052,16 +1080,31 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     PathState ps;
     load_path(in, q, ps);
     const float4 hit = in.hit[q];
+    // The next kSeg positions of the segment's work stream and their pixels:
+    // slot j of the free slots regenerates position cursor + j.  Looked up
+    // here, beside the path loads, and parked in LDS; a lookup after the
+    // compaction would wait for every store and atomic issued before it
+    // (vmcnt counts in issue order).  Work ids < 2^31 (runtime chunking).
+    const uint64_t wspec = stream_work(wd, wd.b0 + b, cursor + tid);
+    const uint32_t pspec = wspec < wd.total ? wd.pixels[(uint32_t)wspec % wd.M] : 0u;
     DevScene S = Sg;
     if (lds_bytes) {
         for (uint32_t i = tid; i < lds_bytes / 16; i += kShadeBlock) blob_lds[i] = Sg.blob[i];
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
     }
+    NORI_SPHASE(0)
     ShadowOut so;
     so.emit = false;
     bool alive = false;
+#ifdef NORI_PROF_SHADE
+    __builtin_amdgcn_s_waitcnt(0);  // path loads landed: phase 1 is the shading proper
+    NORI_SPHASE(0)
+#endif
     if (tid < n_in) alive = shade_vertex<INTEG, true>(S, ps, hit, rec, so);
+    NORI_SPHASE(1)
+    s_w[tid] = wspec < wd.total ? (uint32_t)wspec : ~0u;
+    s_pix[tid] = pspec;
     // ---- compaction: survivors first (in lane order), shadow rays likewise
     const uint64_t mal = __ballot(alive), msh = __ballot(so.emit);
     if (lane_id() == 0) {
@@ -1069,6 +1112,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         s_sh[wave] = (uint32_t)__popcll(msh);
     }
     __syncthreads();
+    NORI_SPHASE(2)
     uint32_t al_off = rank_in(mal), sh_off = rank_in(msh), al_tot = 0, sh_tot = 0;
     for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
         al_off += w < wave ? s_al[w] : 0u;
@@ -1076,6 +1120,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         al_tot += s_al[w];
         sh_tot += s_sh[w];
     }
+    const uint32_t need_tot = kSeg - al_tot;
     if (so.emit) {
         uint32_t i = b * kSeg + sh_off;
         sq.ray_o[i] = make_float4(so.o.x, so.o.y, so.o.z, kEps);
@@ -1084,19 +1129,29 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     }
     if (TRACE && alive) trace_into(Sg, ps, out.hit + b * kSeg + al_off);
     if (alive) store_path(out, b * kSeg + al_off, ps);
+    NORI_SPHASE(3)
     // ---- regeneration: the free slots [al_tot, kSeg) take the next work ids of
     // the segment's stream, so only the tail waves run the camera-ray code and
     // a wave's new samples are adjacent pixels (stream_work increases with p)
-    const uint32_t need_tot = kSeg - al_tot;
     if (tid >= al_tot) {
-        const uint64_t w = stream_work(wd, wd.b0 + b, cursor + (tid - al_tot));
-        if (w < wd.total) {
+        const uint32_t wn = s_w[tid - al_tot];
+        if (wn != ~0u) {
             PathState np;
-            regen_path(Sg, wd, (uint32_t)w, np, rec);
+            regen_path(Sg, wd, wn, s_pix[tid - al_tot], np, rec);
             if (TRACE) trace_into(Sg, np, out.hit + q);
             store_path(out, q, np);
         }
     }
+    NORI_SPHASE(4)
+#ifdef NORI_PROF_SHADE
+    __builtin_amdgcn_s_waitcnt(0);
+    NORI_SPHASE(5)
+    if (lane_id() == 0 && (b & 15) == 0) {  // a sample of the waves (atomics on one line)
+        for (int i = 0; i < 6; ++i) atomicAdd(&C->prof[i], (unsigned long long)pt[i]);
+        atomicAdd(&C->prof[6], 1ull);
+    }
+#endif
+#undef NORI_SPHASE
     if (tid == 0) {
         // new samples = the prefix of [cursor, cursor + need_tot) still inside the stream
         uint32_t lo = 0, hi = need_tot;
@@ -1309,6 +1364,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
     if (active) {
         load_path(Q, q, ps);
         h = Q.hit[q];
+        ps.L = ld3(rec[ps.work]);
     }
     uint32_t rays = 0;
     auto trace = [&](const TRay &r, bool want, bool any_hit, float &t, uint32_t &p, float &u, float &v) -> bool {
@@ -1318,22 +1374,32 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         return any_hit ? traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)
                        : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
     };
+#ifdef NORI_PROF_FINISH  // profiling build: clocks of the loop's phases, summed over waves
+    uint64_t pt[4] = {0, 0, 0, 0}, pc = __builtin_amdgcn_s_memtime();
+#define NORI_PHASE(i)                                        \
+    {                                                        \
+        const uint64_t now = __builtin_amdgcn_s_memtime();   \
+        pt[i] += now - pc;                                   \
+        pc = now;                                            \
+    }
+#else
+#define NORI_PHASE(i)
+#endif
     while (__ballot(active)) {
         ShadowOut so;
         so.emit = false;
         bool alive = false;
         if (active) alive = shade_vertex<INTEG, false>(S, ps, h, rec, so);
+        NORI_PHASE(0)
         {
             TRay r{so.o, so.d, V3{0, 0, 0}, kEps, so.maxt};
             float t, u, v;
             uint32_t p;
             rays += so.emit ? 1u : 0u;
             bool occluded = trace(r, so.emit, true, t, p, u, v);
-            if (so.emit && !occluded) {
-                float4 L = rec[so.work];
-                rec[so.work] = make_float4(L.x + so.contrib.x, L.y + so.contrib.y, L.z + so.contrib.z, L.w);
-            }
+            if (so.emit && !occluded) ps.L = ps.L + so.contrib;  // so.work == ps.work
         }
+        NORI_PHASE(1)
         if (active && !alive) {
             active = false;
             // the sample is complete: splat it (k_splat skipped it as pending)
@@ -1342,7 +1408,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             Pcg rg;
             wave_seed(rg, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
             V2 jit = next2D(rg);
-            splat_sample(Sg, film, C, x, y, jit, rec[w]);  // Sg: kernarg filter table (no local copy)
+            // Sg: kernarg filter table (no local copy)
+            splat_sample(Sg, film, C, x, y, jit, make_float4(ps.L.x, ps.L.y, ps.L.z, 0.0f));
             atomicAdd(&seg.stats[sg].w, rays);
             atomicAdd(&C->finish_paths, 1u);
             atomicMax(&C->finish_max_rays, rays);
@@ -1351,9 +1418,19 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         float t, u, v;
         uint32_t p;
         rays += active ? 1u : 0u;
+        NORI_PHASE(2)
         trace(r, active, false, t, p, u, v);
         if (active) h = make_float4(t, __uint_as_float(p), u, v);
+        NORI_PHASE(3)
+#ifdef NORI_PROF_FINISH
+        if (lane_id() == 0) atomicAdd(&C->prof[4], 1ull);
+#endif
     }
+#ifdef NORI_PROF_FINISH
+    if (lane_id() == 0)
+        for (int i = 0; i < 4; ++i) atomicAdd(&C->prof[i], (unsigned long long)pt[i]);
+#endif
+#undef NORI_PHASE
 }
 
 // ------------------------------------------------------------------ film splat

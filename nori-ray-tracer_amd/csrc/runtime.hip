@@ -830,8 +830,19 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         invalid += hc.invalid;
         if (debug_log())
+        {
             std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays\n", p0,
                          (unsigned long)iters, hc.finish_paths, hc.finish_max_rays);
+            if (hc.prof[6])  // NORI_PROF_SHADE builds
+                std::fprintf(stderr, "[nori] shade clocks per wave: loads %.0f shade %.0f compact %.0f store %.0f regen %.0f drain %.0f (%llu waves)\n",
+                             (double)hc.prof[0] / hc.prof[6], (double)hc.prof[1] / hc.prof[6],
+                             (double)hc.prof[2] / hc.prof[6], (double)hc.prof[3] / hc.prof[6],
+                             (double)hc.prof[4] / hc.prof[6], (double)hc.prof[5] / hc.prof[6], hc.prof[6]);
+            else if (hc.prof[4])  // NORI_PROF_FINISH builds
+                std::fprintf(stderr, "[nori] finisher clocks per wave-iteration: shade %.0f shadow %.0f splat %.0f extend %.0f (%llu)\n",
+                             (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4],
+                             (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
+        }
         done_before += wd.total;
     }
     if (samples_started != done_before && !cancelled)
