@@ -9,6 +9,12 @@ namespace nori {
 constexpr int kShadeBlock = 256;   // shade / regen work-group size
 constexpr int kTraceBlock = 128;   // traversal work-group size (LDS stack columns)
 constexpr int kTraceSpill = 64;    // traversal stack entries beyond the LDS part (private memory)
+#ifndef NORI_STACK_KEYS
+#define NORI_STACK_KEYS 1
+#endif
+// Stack entries held in LDS for an LDS budget of `stack` words per lane: with
+// NORI_STACK_KEYS each entry is a (child ref, entry distance) pair.
+constexpr int stack_lds_entries(int stack) { return NORI_STACK_KEYS ? stack / 2 : stack; }
 #ifndef NORI_TRACE_GROUP
 #define NORI_TRACE_GROUP 4
 #endif

@@ -215,6 +215,11 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
     }
 }
 
+// LDS words per lane of a traversal stack of depth STACK: child refs and entry distances.
+// (stack_lds_entries(STACK) entries: the LDS budget stays STACK words, so the
+// occupancy does not change; deeper entries spill to private memory)
+constexpr int stack_words(int STACK) { return STACK ? STACK : 1; }
+
 // BVH::rayIntersect (bvh.cpp:404-462): adaptive epsilon, closest or any hit.
 // Near child first; the short stack lives in LDS, one column per lane.
 template <int STACK, bool ANY>
@@ -241,10 +246,21 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     // push the others farthest first.  Box tests are monotone (a child box lies
     // inside its parent's and rounding keeps the slab test monotone), so the
     // candidate primitives are exactly those of the reference's binary tree.
+    // Stack entries carry the child's entry distance: a popped entry whose box
+    // starts beyond the current closest hit is dropped unvisited -- exactly
+    // the nearT <= maxt clause of its box test re-run at pop time (same ray,
+    // same box, maxt only shrinks), without fetching the node.
     uint32_t spill[kTraceSpill];  // stack entries beyond the LDS part (rare)
-    auto push = [&](int &sp, uint32_t v) {
-        if (sp < STACK) stk[sp * kTraceBlock] = v;
-        else spill[sp - STACK] = v;
+    float spillk[kTraceSpill];
+    constexpr int L = stack_lds_entries(STACK);
+    auto push = [&](int &sp, uint32_t v, float k) {
+        if (sp < L) {
+            stk[sp * kTraceBlock] = v;
+            if (NORI_STACK_KEYS) stk[(L + sp) * kTraceBlock] = __float_as_uint(k);
+        } else {
+            spill[sp - L] = v;
+            if (NORI_STACK_KEYS) spillk[sp - L] = k;
+        }
         ++sp;
     };
     uint32_t ref = 0;
@@ -292,9 +308,9 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
                 cs(k0, c0, m0, k2, c2, m2);
                 cs(k1, c1, m1, k3, c3, m3);
                 cs(k1, c1, m1, k2, c2, m2);
-                if (nh > 3) push(sp, c3);
-                if (nh > 2) push(sp, c2);
-                if (nh > 1) push(sp, c1);
+                if (nh > 3) push(sp, c3, k3);
+                if (nh > 2) push(sp, c2, k2);
+                if (nh > 1) push(sp, c1, k1);
                 ref = c0;
                 continue;
             }
@@ -322,9 +338,21 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
                 }
             }
         }
-        if (sp == 0) break;
-        --sp;
-        ref = sp < STACK ? stk[sp * kTraceBlock] : spill[sp - STACK];
+        bool next = false;
+        while (sp > 0) {
+            --sp;
+            ref = sp < L ? stk[sp * kTraceBlock] : spill[sp - L];
+            if (!NORI_STACK_KEYS) {
+                next = true;
+                break;
+            }
+            const float key = sp < L ? __uint_as_float(stk[(L + sp) * kTraceBlock]) : spillk[sp - L];
+            if (!(key > r.maxt)) {
+                next = true;
+                break;
+            }
+        }
+        if (!next) break;
     }
     (void)STACK;
     return found;
@@ -332,7 +360,7 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
 
 template <int STACK, bool ANY>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 *rays, uint32_t n, float4 *hits) {
-    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     uint32_t q = blockIdx.x * kTraceBlock + threadIdx.x;
     if (q >= n) return;
     float4 a = rays[2 * (size_t)q], b = rays[2 * (size_t)q + 1];
@@ -433,15 +461,20 @@ ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *sh
     }
 }
 
+#ifdef NORI_TRACE_WAVES
+#define NORI_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(NORI_TRACE_WAVES)))
+#else
+#define NORI_TRACE_ATTR
+#endif
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
-    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     extend_body<STACK>(S, pq, cnt, G, blockIdx.x, stk);
 }
 template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
+__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
                                                         float4 *rec, uint32_t G) {
-    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, blockIdx.x, stk);
 }
 // Scan-mode traversal of K rays per thread: every primitive record is
@@ -1325,7 +1358,7 @@ template <int STACK, int INTEG>
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
                                                         const uint32_t *pre, uint32_t G) {
-    __shared__ uint32_t stk[(STACK ? STACK : 1) * kTraceBlock];
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     // the queued paths of all segments, numbered through the prefix `pre`
     // (k_tail_prefix) so that they fill whole waves: few waves, each with a

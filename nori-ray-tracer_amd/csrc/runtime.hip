@@ -388,10 +388,17 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     // traversal stack: at most 3 entries per level of the 4-wide tree; the
     // first `stack` live in LDS, up to kTraceSpill more in private memory
     const uint32_t need = 3 * bvh.depth + 1;
-    if (need <= 8) c.stack = 8;
-    else if (need <= 16) c.stack = 16;
+    // (LDS budget 16 words: measured best on the 22.7k and 524k triangle
+    // scenes -- occupancy beats a deeper LDS part; 32 only when the spill
+    // area could not cover the rest)
+    if (need <= (uint32_t)stack_lds_entries(8)) c.stack = 8;
+    else if (need <= (uint32_t)stack_lds_entries(16) + kTraceSpill) c.stack = 16;
     else c.stack = 32;
-    if (need > (uint32_t)c.stack + kTraceSpill) throw NoriException(NORI_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
+    if (const char *e = std::getenv("NORI_BVH_STACK")) {  // tuning: 8, 16 or 32
+        const int v = std::atoi(e);
+        if (v == 8 || v == 16 || v == 32) c.stack = v;
+    }
+    if (need > (uint32_t)stack_lds_entries(c.stack) + kTraceSpill) throw NoriException(NORI_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
     // Traversal strategy: scenes of at most kScanMaxPrims primitives are
     // intersected by a wave-uniform scan (scalar loads, no divergence), larger
     // ones by per-lane BVH traversal.  NORI_TRAVERSAL=bvh|scan overrides.
