@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define NORI_GPU_ABI_VERSION 1
+#define NORI_GPU_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define NORI_OK               0
@@ -60,11 +60,32 @@ enum {
     NORI_BSDF_MICROFACET = 3, /* "microfacet" src/microfacet.cpp */
     NORI_BSDF_DISNEY = 4      /* "disney"     src/disney.cpp     */
 };
-enum { NORI_EMITTER_AREA = 0 /* "area" */, NORI_EMITTER_ENVMAP = 1 /* "envmap" */ };
+enum {
+    NORI_EMITTER_AREA = 0,    /* "area"      src/arealight.cpp  */
+    NORI_EMITTER_ENVMAP = 1,  /* "envmap"    src/envmap.cpp     */
+    NORI_EMITTER_POINT = 2,   /* "point"     src/pointlight.cpp */
+    NORI_EMITTER_SPOT = 3     /* "spotlight" src/spotlight.cpp  */
+};
+enum {
+    NORI_TEXTURE_CONSTANT = 0,     /* "constant_color"     src/consttexture.cpp */
+    NORI_TEXTURE_CHECKERBOARD = 1  /* "checkerboard_color" src/checkerboard.cpp */
+};
+enum {
+    NORI_CAMERA_PERSPECTIVE = 0,   /* "perspective"    src/perspective.cpp    */
+    NORI_CAMERA_THINLENS = 1,      /* "thinlens"       src/thinlens.cpp       */
+    NORI_CAMERA_ADVANCED = 2       /* "advancedCamera" src/advancedCamera.cpp */
+};
 enum {
     NORI_INTEGRATOR_PATH_MATS = 0,  /* "path_mats"  src/path_mats.cpp  */
     NORI_INTEGRATOR_PATH_MIS = 1,   /* "path_mis"   src/path_mis.cpp   */
-    NORI_INTEGRATOR_VOLUMETRIC = 2  /* "volumetric" src/volumetric.cpp */
+    NORI_INTEGRATOR_VOLUMETRIC = 2, /* "volumetric" src/volumetric.cpp */
+    /* one-bounce integrators (a fixed number of rays per camera sample) */
+    NORI_INTEGRATOR_NORMALS = 3,    /* "normals"     src/normals.cpp           */
+    NORI_INTEGRATOR_AV = 4,         /* "av"          src/averagevisibility.cpp */
+    NORI_INTEGRATOR_DIRECT = 5,     /* "direct"      src/direct.cpp            */
+    NORI_INTEGRATOR_DIRECT_EMS = 6, /* "direct_ems"  src/direct_ems.cpp        */
+    NORI_INTEGRATOR_DIRECT_MATS = 7,/* "direct_mats" src/direct_mats.cpp       */
+    NORI_INTEGRATOR_DIRECT_MIS = 8  /* "direct_mis"  src/direct_mis.cpp        */
 };
 enum {
     NORI_FILTER_GAUSSIAN = 0, NORI_FILTER_MITCHELL = 1, NORI_FILTER_TENT = 2,
@@ -106,6 +127,10 @@ typedef struct nori_bsdf_desc {
     float kd[3];                  /* microfacet                                */
     float base_color[3];          /* disney                                    */
     float metallic, specular, roughness, sheen, sheen_tint, specular_tint;
+    int32_t albedo_texture;       /* diffuse: NORI_TEXTURE_* of the albedo; a
+                                     checkerboard uses albedo as value1        */
+    float tex_value2[3];          /* checkerboard value2                        */
+    float tex_delta[2], tex_scale[2]; /* checkerboard delta (def 0), scale (def 1) */
 } nori_bsdf_desc;
 
 typedef struct nori_emitter_desc {
@@ -116,6 +141,11 @@ typedef struct nori_emitter_desc {
     float lum_scale[3];           /* envmap luminanceScale                     */
     int32_t env_rows, env_cols;   /* envmap: Bitmap rows x cols                */
     const float *env_rgb;         /* envmap: rows*cols*3 floats (row-major)    */
+    float position[3];            /* point / spot                              */
+    float power[3];               /* point: power | spot: color                */
+    float direction[3];           /* spot: normalized direction                */
+    float cos_falloff_start;      /* spot: cos(falloffStart deg)               */
+    float cos_total_width;        /* spot: cos(totalWidth deg)                 */
 } nori_emitter_desc;
 
 typedef struct nori_camera_desc {
@@ -126,6 +156,11 @@ typedef struct nori_camera_desc {
     int32_t filter_type;          /* NORI_FILTER_*                             */
     float filter_radius;
     float filter_p0, filter_p1;   /* gaussian: stddev | mitchell: B, C | windowed: tau */
+    int32_t camera_type;          /* NORI_CAMERA_*                             */
+    float lens_radius;            /* thinlens / advancedCamera "lensRadius"    */
+    float focal_distance;         /* "focalDist"                               */
+    float distortion[2];          /* advancedCamera barrel distortion k1, k2   */
+    float chromatic[3];           /* advancedCamera "chromaticAberation"       */
 } nori_camera_desc;
 
 typedef struct nori_medium_desc {
@@ -152,6 +187,7 @@ typedef struct nori_scene_desc {
     nori_medium_desc medium;
     int32_t integrator;           /* NORI_INTEGRATOR_*                          */
     uint32_t sample_count;        /* independent sampler sampleCount = spp      */
+    float av_length;              /* "av" integrator ray length                 */
 } nori_scene_desc;
 
 /* ---- host-side scene loading (the plugin boundary) ----------------------- */

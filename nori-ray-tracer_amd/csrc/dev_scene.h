@@ -2,10 +2,10 @@
 //
 // HBM layout (all arrays 16-byte aligned, structure-of-arrays so a wave's
 // 64 lanes read/write 64 consecutive 16-byte records = 1 KiB per access):
-//   nodes      float4[4*N]   BVH, 64 B per inner node (host_scene.h)
+//   nodes      float4[8*N]   4-wide BVH, 128 B per inner node (host_scene.h)
 //   prims      float4[3*P]   48 B per primitive in leaf order
 //   tri_vidx   uint32[3*P]   vertex ids per global primitive (shading)
-//   pos, nrm   float4[V]     vertex position / normal (w unused)
+//   pos, nrm   float4[V]     vertex position + texture u / normal + texture v
 //   prim_shape uint32[P]     global primitive -> shape
 //   cdf        float[]       per-mesh area CDFs (DiscretePDF, dpdf.h)
 // Path queues (two, ping-ponged) hold one path per entry:
@@ -24,23 +24,27 @@ namespace nori {
 
 struct DevShape {
     int32_t type, bsdf, emitter, has_normals;
-    uint32_t prim_offset, prim_count, cdf_offset, pad;
+    uint32_t prim_offset, prim_count, cdf_offset, has_uvs;
     float center[3], radius;
     float area_norm;     // DiscretePDF::getNormalization (mesh) or sphere pdf
     float pad2[3];
 };
 
-// 64 B.  Area: radiance.  Envmap (envmap.cpp): R x C texels (R = Bitmap rows,
+// 128 B.  Area: radiance.  Envmap (envmap.cpp): R x C texels (R = Bitmap rows,
 // the reference's m_width), tables at float offsets into DevScene::env:
 // rgb R*C*3, pdf R*C, cdf R*(C+1), marginal pdf R, marginal cdf R+1.
+// Point (pointlight.cpp): position, power.  Spot (spotlight.cpp): position,
+// power (= "color"), direction, cosines of falloffStart and totalWidth.
 struct DevEmitter {
     int32_t type, shape;
     float radiance[3];
     float weight;
     int32_t R, C;
     uint32_t rgb_off, pdf_off, cdf_off, pmarg_off, cmarg_off;
-    uint32_t pad[3];
+    float position[3], power[3], direction[3], cos_fs, cos_tw;
+    uint32_t pad[8];
 };
+static_assert(sizeof(DevEmitter) == 128, "DevEmitter layout");
 
 struct DevScene {
     const float4 *nodes;
@@ -65,6 +69,12 @@ struct DevScene {
     float c2w[16];
     float cam_o[3];  // cameraToWorld * (0,0,0,1) / w (perspective.cpp:104)
     float near_clip, far_clip;
+    int32_t cam_type;          // NORI_CAMERA_*
+    float lens_radius, focal;  // thinlens / advancedCamera
+    float distortion[2];       // advancedCamera barrel distortion
+    float chromatic[3];        // advancedCamera chromatic aberration (path kernels: zero)
+    int32_t W_max;             // max(W, H)
+    float av_length;           // "av" integrator
     float filter[NORI_FILTER_RESOLUTION + 1];
     float filter_radius, lookup;
     int32_t border;
@@ -167,6 +177,8 @@ struct Counters {
     uint32_t finish_paths;         // paths completed by the tail finisher
     uint32_t finish_max_rays;      // most rays traced by one finisher path
     uint32_t pad2[30];
+    unsigned long long direct_rays[2];  // one-bounce integrators: closest-hit, shadow rays
+    unsigned long long pad3[14];
 };
 
 }  // namespace nori

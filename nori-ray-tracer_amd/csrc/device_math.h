@@ -161,6 +161,24 @@ NHD V3 sq_beckmann(V2 s, float alpha) {  // warp.cpp:122-127 (pow(alpha,2) is do
     float st = sinf(theta);
     return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
 }
+// Warp::squareToConcentricDisk (warp.cpp:143-162), squareToUniformDisk (warp.cpp:53-58)
+NHD V2 sq_concentric_disk(V2 s) {
+    const V2 o = V2{2.f * s.x - 1.f, 2.f * s.y - 1.f};
+    if (o.x == 0.0f && o.y == 0.0f) return V2{0, 0};
+    float theta, r;
+    if (fabsf(o.x) > fabsf(o.y)) {
+        r = o.x;
+        theta = kPi * 0.25f * (o.y / o.x);
+    } else {
+        r = o.y;
+        theta = kPi * 0.5f - kPi * 0.25f * (o.x / o.y);
+    }
+    return V2{r * cosf(theta), r * sinf(theta)};
+}
+NHD V2 sq_uniform_disk(V2 s) {
+    const float angle = 2 * s.x * kPi, size = sqrtf(s.y);
+    return V2{cosf(angle) * size, sinf(angle) * size};
+}
 NHD V3 sq_uniform_triangle(V2 s) {  // warp.cpp:135-140
     float su1 = sqrtf(s.x);
     float u = 1.f - su1, v = s.y * su1;
@@ -192,12 +210,24 @@ struct DevBsdf {
     float kd[3];
     float base[3];
     float metallic, specular, roughness, sheen, sheen_tint, spec_tint, d_alpha;
+    int32_t tex;  // diffuse albedo: NORI_TEXTURE_CONSTANT (albedo) or _CHECKERBOARD (albedo = value1)
+    float tex_v2[3], tex_delta[2], tex_scale[2];
 };
 
 struct BRec {
     V3 wi, wo;
     int measure;
+    V2 uv;  // bsdf.h:55, the hit's texture coordinates
 };
+
+// Texture<Color3f>::eval: constant (consttexture.cpp) or Checkerboard::eval
+// (checkerboard.cpp:22-27)
+ND V3 albedo_at(const DevBsdf &b, V2 uv) {
+    if (b.tex != NORI_TEXTURE_CHECKERBOARD) return V3{b.albedo[0], b.albedo[1], b.albedo[2]};
+    const int x = (int)fabsf(floorf(uv.x / b.tex_scale[0] - b.tex_delta[0]));
+    const int y = (int)fabsf(floorf(uv.y / b.tex_scale[1] - b.tex_delta[1]));
+    return x % 2 == y % 2 ? V3{b.albedo[0], b.albedo[1], b.albedo[2]} : V3{b.tex_v2[0], b.tex_v2[1], b.tex_v2[2]};
+}
 
 ND float beckmann_D(const DevBsdf &b, V3 m) {  // microfacet.cpp:47-53
     float temp = tan_theta(m) / b.alpha, ct = m.z, ct2 = ct * ct;
@@ -227,7 +257,7 @@ ND V3 bsdf_eval(const DevBsdf &b, const BRec &r) {
     switch (b.type) {
     case NORI_BSDF_DIFFUSE:  // diffuse.cpp:72-82
         if (r.measure != kMeasureSolidAngle || r.wi.z <= 0 || r.wo.z <= 0) return V3{0, 0, 0};
-        return V3{b.albedo[0], b.albedo[1], b.albedo[2]} * kInvPi;
+        return albedo_at(b, r.uv) * kInvPi;
     case NORI_BSDF_MICROFACET: {  // microfacet.cpp:79-90
         V3 n = normalize(r.wi + r.wo);
         float D = beckmann_D(b, n);
@@ -297,7 +327,7 @@ ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
         if (r.wi.z <= 0) return V3{0, 0, 0};
         r.measure = kMeasureSolidAngle;
         r.wo = sq_cosine_hemisphere(s);
-        return V3{b.albedo[0], b.albedo[1], b.albedo[2]};
+        return albedo_at(b, r.uv);
     case NORI_BSDF_MIRROR:  // mirror.cpp:39-55
         if (r.wi.z <= 0) return V3{0, 0, 0};
         r.wo = V3{-r.wi.x, -r.wi.y, r.wi.z};

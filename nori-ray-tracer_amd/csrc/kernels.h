@@ -57,6 +57,9 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                          hipStream_t st);
+// One-bounce integrators (normals, av, direct, direct_ems/mats/mis): one thread
+// per work id of wd (pass-major, pixels in wd.pixels order) writes its record.
+hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack, hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 

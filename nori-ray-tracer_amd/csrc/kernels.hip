@@ -560,22 +560,35 @@ struct SurfHit {
     V3 p;
     Frame sh;
     int shape;
+    V2 uv;
 };
 
-// setHitInformation: mesh.cpp:122-170, sphere.cpp:78-93 (shading frame only).
+// setHitInformation: mesh.cpp:122-170, sphere.cpp:78-93 (shading frame and
+// texture coordinates; a mesh without UVs keeps the barycentrics in its.uv).
 ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, V3 o, V3 d) {
     SurfHit h;
     h.shape = (int)S.prim_shape[prim];
     const DevShape &sh = S.shapes[h.shape];
     if (sh.type == NORI_SHAPE_SPHERE) {
         h.p = o + d * t;
-        h.sh = frame_from(normalize(h.p - V3{sh.center[0], sh.center[1], sh.center[2]}));
+        const V3 n = normalize(h.p - V3{sh.center[0], sh.center[1], sh.center[2]});
+        h.sh = frame_from(n);
+        // sphericalCoordinates (common.cpp:264-272); 0.5 is a double literal
+        float phi = atan2f(n.y, n.x);
+        if (phi < 0) phi += 2 * kPi;
+        h.uv.x = (float)(0.5 + (double)(acosf(n.z) / (2 * kPi)));
+        h.uv.y = phi / kPi;
     } else {
         const uint32_t *f = S.tri_vidx + 3 * (size_t)prim;
         uint32_t i0 = f[0], i1 = f[1], i2 = f[2];
-        V3 p0 = ld3(S.pos[i0]), p1 = ld3(S.pos[i1]), p2 = ld3(S.pos[i2]);
+        const float4 q0 = S.pos[i0], q1 = S.pos[i1], q2 = S.pos[i2];
+        V3 p0 = ld3(q0), p1 = ld3(q1), p2 = ld3(q2);
         float bx = 1 - (u + v);
         h.p = (p0 * bx + p1 * u) + p2 * v;
+        h.uv = V2{u, v};
+        if (sh.has_uvs)  // u in pos.w, v in nrm.w
+            h.uv = V2{(bx * q0.w + u * q1.w) + v * q2.w,
+                      (bx * S.nrm[i0].w + u * S.nrm[i1].w) + v * S.nrm[i2].w};
         if (sh.has_normals) {
             V3 n = (ld3(S.nrm[i0]) * bx + ld3(S.nrm[i1]) * u) + ld3(S.nrm[i2]) * v;
             h.sh = frame_from(normalize(n));
@@ -692,19 +705,68 @@ ND void sample_surface(const DevScene &S, const DevShape &sh, V2 smp, V3 &p, V3 
         n = normalize(cross(p1 - p0, p2 - p0));
 }
 
-ND void camera_ray(const DevScene &S, float px, float py, V3 &o, V3 &d, float &mint, float &maxt) {
-    // PerspectiveCamera::sampleRay (perspective.cpp:90-112); Eigen column order.
+// Camera::sampleRay: PerspectiveCamera (perspective.cpp:90-112), ThinLensCamera
+// (thinlens.cpp:120-147) and AdvancedCamera (advancedCamera.cpp:85-157: barrel
+// distortion, uniform-disk lens, per-channel focus shift with chromatic
+// aberration, channel = 0..2 then; -1 otherwise).  Eigen column order.
+ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel, V3 &o, V3 &d, float &mint,
+                      float &maxt) {
     const float *m = S.s2c;
-    float qx = px * S.invW, qy = py * S.invH;
-    float r0 = ((m[0] * qx + m[1] * qy) + m[2] * 0.0f) + m[3];
-    float r1 = ((m[4] * qx + m[5] * qy) + m[6] * 0.0f) + m[7];
-    float r2 = ((m[8] * qx + m[9] * qy) + m[10] * 0.0f) + m[11];
-    float r3 = ((m[12] * qx + m[13] * qy) + m[14] * 0.0f) + m[15];
+    const float qx = px * S.invW, qy = py * S.invH;
+    const float r0 = ((m[0] * qx + m[1] * qy) + m[2] * 0.0f) + m[3];
+    const float r1 = ((m[4] * qx + m[5] * qy) + m[6] * 0.0f) + m[7];
+    const float r2 = ((m[8] * qx + m[9] * qy) + m[10] * 0.0f) + m[11];
+    const float r3 = ((m[12] * qx + m[13] * qy) + m[14] * 0.0f) + m[15];
     V3 nearP = V3{r0 / r3, r1 / r3, r2 / r3};
     V3 dl = normalize(nearP);
-    float invZ = 1.0f / dl.z;
+    float w = 0.0f;
+    bool chroma = false;
+    if (S.cam_type == NORI_CAMERA_ADVANCED) {
+        const float k1 = S.distortion[0], k2 = S.distortion[1];
+        if (k1 != 0.0f || k2 != 0.0f) {  // Newton iterations for the undistorted radius
+            const float ux = nearP.x / nearP.z, uy = nearP.y / nearP.z;
+            const float y = sqrtf(ux * ux + uy * uy);
+            float r = y, rr, f, df;
+            int i = 0;
+            for (;;) {
+                rr = r * r;
+                f = r * (1 + (k1 * rr) + k2 * (rr * rr)) - y;
+                df = 1 + (3 * k1 * rr) + (5 * k2 * rr * rr);
+                r = r - f / df;
+                if ((double)fabsf(f) < 1e-6 || i++ > 4) break;
+            }
+            const float factor = r / y;
+            nearP.x *= factor;
+            nearP.y *= factor;
+            dl = normalize(nearP);
+        }
+        chroma = S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f;
+        if (chroma) w = S.chromatic[channel < 0 ? 0 : (channel > 2 ? 2 : channel)];
+    }
+    const float invZ = 1.0f / dl.z;
     const float *c = S.c2w;
-    o = V3{S.cam_o[0], S.cam_o[1], S.cam_o[2]};  // cameraToWorld * (0,0,0,1), same for every ray (host)
+    V3 lo = V3{0, 0, 0};
+    if (S.cam_type != NORI_CAMERA_PERSPECTIVE && (S.lens_radius > 0.0f || chroma)) {
+        V2 pl = S.cam_type == NORI_CAMERA_THINLENS ? sq_concentric_disk(ap) : sq_uniform_disk(ap);
+        pl = V2{S.lens_radius * pl.x, S.lens_radius * pl.y};
+        const float ft = S.focal / dl.z;
+        V3 pf = dl * ft;  // Ray3f(0, d)(ft)
+        if (S.cam_type == NORI_CAMERA_ADVANCED) {
+            float spx = px - 0.5f * (float)S.W, spy = py - 0.5f * (float)S.H;
+            spx /= (float)S.W_max;
+            spy /= (float)S.W_max;
+            const float sq = spx * spx + spy * spy;
+            pf = pf + V3{-((spx * sq) * w), (spy * sq) * w, 0.0f};
+        }
+        lo = V3{pl.x, pl.y, 0.0f};
+        dl = normalize(pf - lo);
+        const float hw = ((c[12] * lo.x + c[13] * lo.y) + c[14] * lo.z) + c[15];
+        o = V3{(((c[0] * lo.x + c[1] * lo.y) + c[2] * lo.z) + c[3]) / hw,
+               (((c[4] * lo.x + c[5] * lo.y) + c[6] * lo.z) + c[7]) / hw,
+               (((c[8] * lo.x + c[9] * lo.y) + c[10] * lo.z) + c[11]) / hw};
+    } else {
+        o = V3{S.cam_o[0], S.cam_o[1], S.cam_o[2]};  // cameraToWorld * (0,0,0,1), same for every ray (host)
+    }
     d = V3{(c[0] * dl.x + c[1] * dl.y) + c[2] * dl.z, (c[4] * dl.x + c[5] * dl.y) + c[6] * dl.z,
            (c[8] * dl.x + c[9] * dl.y) + c[10] * dl.z};
     mint = S.near_clip * invZ;
@@ -811,23 +873,45 @@ ND bool medium_sample(const DevScene &S, V3 o, V3 d, Pcg &rng, float tmax, V3 &p
     return true;
 }
 
+// PointLight::sample (pointlight.cpp:17-25) and SpotLight::sample
+// (spotlight.cpp:20-46, falloff by the angle to the spot direction) from x:
+// returns the radiance, sets the direction and the shadow ray's maxt.
+ND V3 point_sample(const DevEmitter &E, V3 x, V3 &wi, float &maxt) {
+    const V3 pos = V3{E.position[0], E.position[1], E.position[2]};
+    const V3 d = pos - x;
+    wi = normalize(d);
+    maxt = norm(d) - kEps;
+    const V3 pw = V3{E.power[0], E.power[1], E.power[2]};
+    if (E.type == NORI_EMITTER_POINT) return pw / (4.f * kPi * dot(d, d));
+    const V3 w = -wi, dir = V3{E.direction[0], E.direction[1], E.direction[2]};
+    const float cosTheta = dot(dir, normalize(w));
+    float fo;
+    if (cosTheta < E.cos_tw) fo = 0;
+    else if (cosTheta > E.cos_fs) fo = 1;
+    else fo = (acosf(E.cos_tw) - acosf(cosTheta)) / (acosf(E.cos_tw) - acosf(E.cos_fs));
+    const V3 q = x - pos;
+    return (pw * fo) / (4.f * kPi * dot(q, q));
+}
+
 // Next-event estimation from x (AreaEmitter::sample, arealight.cpp:52-68):
 // one emitter chosen uniformly (scene.h:68-74), Li already scaled by N.
 struct NeeSample {
     V3 p, wi, Li;
     float pdf_em, maxt;  // maxt: of the shadow ray from x
 };
-ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
+// Emitter::sample of one emitter from x with the 2D sample s2: radiance over
+// pdf (not yet scaled by the emitter count), direction, area-measure pdf and
+// the shadow ray's maxt.
+ND NeeSample emitter_sample_one(const DevScene &S, const DevEmitter &E, V3 x, V2 s2) {
     NeeSample r;
-    const float ul = next1D(rng);
-    const uint32_t N = S.num_emitters;
-    uint32_t li = (uint32_t)floorf((float)N * ul);
-    if (li > N - 1) li = N - 1;
-    const DevEmitter &E = S.emitters[li];
-    const V2 s2 = next2D(rng);
+    if (E.type == NORI_EMITTER_POINT || E.type == NORI_EMITTER_SPOT) {
+        r.Li = point_sample(E, x, r.wi, r.maxt);
+        r.pdf_em = 1.0f;  // PDF_VALUE (pointlight.cpp:32-35) / lRec.pdf (spotlight.cpp:54-57)
+        r.p = V3{E.position[0], E.position[1], E.position[2]};
+        return r;
+    }
     if (E.type == NORI_EMITTER_ENVMAP) {
-        const V3 Li = env_sample(S, E, s2, r.wi);
-        r.Li = Li * (float)N;
+        r.Li = env_sample(S, E, s2, r.wi);
         r.pdf_em = env_pdf(S, E, r.wi);
         r.maxt = kEnvTFar;               // shadow ray (ref, wi, Epsilon, T_FAR)
         r.p = x + r.wi * kEnvTFar;       // D4: lRec.p is never set by the reference
@@ -839,9 +923,20 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
     r.wi = normalize(dv);
     r.pdf_em = emitter_pdf(S, E, ln, r.wi);
     const float att = dot(ln, -r.wi) / dot(dv, dv);
-    V3 Li = r.pdf_em > 0.0f ? (emitter_eval(S, E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
-    r.Li = Li * (float)N;
+    r.Li = r.pdf_em > 0.0f ? (emitter_eval(S, E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
     r.maxt = norm(dv) - kEps;
+    return r;
+}
+// Next-event estimation of the path integrators: one emitter chosen uniformly
+// (Scene::getRandomEmitter, scene.h:68-74), Li scaled by the emitter count.
+ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
+    const float ul = next1D(rng);
+    const uint32_t N = S.num_emitters;
+    uint32_t li = (uint32_t)floorf((float)N * ul);
+    if (li > N - 1) li = N - 1;
+    const V2 s2 = next2D(rng);
+    NeeSample r = emitter_sample_one(S, S.emitters[li], x, s2);
+    r.Li = r.Li * (float)N;
     return r;
 }
 
@@ -933,6 +1028,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
         NeeSample ne = nee_sample(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
+        br.uv = hs.uv;
         br.wo = to_local(hs.sh, ne.wi);
         br.measure = kMeasureSolidAngle;
         const float theta = smax(0.0f, br.wo.z);
@@ -952,6 +1048,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     ps.beta = ps.beta / q;
     BRec br;
     br.wi = to_local(hs.sh, -ps.d);
+    br.uv = hs.uv;
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
     const V3 w = bsdf_sample(B, br, next2D(ps.rng));
@@ -1005,6 +1102,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         const NeeSample ne = nee_sample(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
+        br.uv = hs.uv;
         br.wo = to_local(hs.sh, ne.wi);
         br.measure = kMeasureSolidAngle;
         float theta = smax(0.0f, br.wo.z);
@@ -1024,6 +1122,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     ps.beta = ps.beta / qrr;
     BRec br;
     br.wi = to_local(hs.sh, -ps.d);
+    br.uv = hs.uv;
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
 #ifdef NORI_PROF_NO_SAMPLE  // profiling build only: a cheap reflection instead of BSDF sampling
@@ -1057,8 +1156,8 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t p
     uint64_t sid = (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix;
     wave_seed(ps.rng, wd.seed, sid);
     V2 jit = next2D(ps.rng);
-    (void)next2D(ps.rng);  // apertureSample (render.cpp:99)
-    camera_ray(S, (float)x + jit.x, (float)y + jit.y, ps.o, ps.d, ps.mint, ps.maxt);
+    const V2 ap = next2D(ps.rng);  // apertureSample (render.cpp:99)
+    camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, -1, ps.o, ps.d, ps.mint, ps.maxt);
     ps.beta = V3{1, 1, 1};
     ps.prev = -1.0f;
     ps.work = w;
@@ -1466,6 +1565,158 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
 #undef NORI_PHASE
 }
 
+// ------------------------------------------------------------------ one-bounce integrators
+// normals (normals.cpp:16-24), av (averagevisibility.cpp:16-27), direct
+// (direct.cpp:17-45), direct_ems (direct_ems.cpp:17-51), direct_mats
+// (direct_mats.cpp:17-44), direct_mis (direct_mis.cpp:17-85).  They trace a
+// fixed, small number of rays per camera sample (1 + lights + 1 at most), so
+// there is no path state to keep: one thread runs one sample start to end and
+// writes its record; k_splat filters the records as for the path integrators.
+template <int STACK>
+struct OneBounce {
+    const DevScene &S;
+    uint32_t *stk;
+    uint32_t rc = 0, rs = 0;  // rays traced: closest, shadow
+    ND bool closest(V3 o, V3 d, float mint, float maxt, SurfHit &hs) {
+        ++rc;
+        TRay r{o, d, V3{0, 0, 0}, mint, maxt};
+        float t, u, v;
+        uint32_t p;
+        if (!traverse<STACK, false>(S, r, stk, t, p, u, v)) return false;
+        hs = surface(S, p, t, u, v, o, d);
+        return true;
+    }
+    ND bool occluded(V3 o, V3 d, float maxt) {
+        ++rs;
+        TRay r{o, d, V3{0, 0, 0}, kEps, maxt};
+        float t, u, v;
+        uint32_t p;
+        return traverse<STACK, true>(S, r, stk, t, p, u, v);
+    }
+    // emission of the hit surface seen from `from` (EmitterQueryRecord(from, its.p, n))
+    ND V3 emission(const SurfHit &hs, V3 from) {
+        const DevShape &sh = S.shapes[hs.shape];
+        if (sh.emitter < 0) return V3{0, 0, 0};
+        return emitter_eval(S, S.emitters[sh.emitter], hs.sh.n, normalize(hs.p - from));
+    }
+    template <int INTEG>
+    ND V3 Li(Pcg &rng, V3 o, V3 d, float mint, float maxt) {
+        SurfHit hs;
+        if (!closest(o, d, mint, maxt, hs)) return INTEG == NORI_INTEGRATOR_AV ? V3{1, 1, 1} : V3{0, 0, 0};
+        if (INTEG == NORI_INTEGRATOR_NORMALS) return V3{fabsf(hs.sh.n.x), fabsf(hs.sh.n.y), fabsf(hs.sh.n.z)};
+        if (INTEG == NORI_INTEGRATOR_AV) {
+            // Warp::sampleUniformHemisphere (warp.cpp:25-42): rejection in the cube
+            V3 w;
+            do {
+                w.x = 1.f - 2.f * next1D(rng);
+                w.y = 1.f - 2.f * next1D(rng);
+                w.z = 1.f - 2.f * next1D(rng);
+            } while (dot(w, w) > 1.f);
+            if (dot(w, hs.sh.n) < 0.f) w = -w;
+            w = w / norm(w);
+            ++rs;
+            TRay r{hs.p, w, V3{0, 0, 0}, kEps, S.av_length};
+            float t, u, v;
+            uint32_t p;
+            return traverse<STACK, true>(S, r, stk, t, p, u, v) ? V3{0, 0, 0} : V3{1, 1, 1};
+        }
+        const DevBsdf &B = S.bsdfs[S.shapes[hs.shape].bsdf];
+        V3 color = INTEG == NORI_INTEGRATOR_DIRECT ? V3{0, 0, 0} : emission(hs, o);
+        if (INTEG == NORI_INTEGRATOR_DIRECT || INTEG == NORI_INTEGRATOR_DIRECT_EMS ||
+            INTEG == NORI_INTEGRATOR_DIRECT_MIS) {
+            // every light, one shadow ray each; `direct` passes an unset sample
+            // (its lights ignore it): (0, 0) here, nothing drawn
+            for (uint32_t i = 0; i < S.num_emitters; ++i) {
+                const V2 s2 = INTEG == NORI_INTEGRATOR_DIRECT ? V2{0, 0} : next2D(rng);
+                const NeeSample ne = emitter_sample_one(S, S.emitters[i], hs.p, s2);
+                if (occluded(hs.p, ne.wi, ne.maxt)) continue;
+                const V3 wi = to_local(hs.sh, ne.wi), dv = to_local(hs.sh, -d);
+                BRec br;
+                br.measure = kMeasureSolidAngle;
+                br.uv = hs.uv;
+                br.wi = INTEG == NORI_INTEGRATOR_DIRECT ? wi : dv;  // direct.cpp builds (light, view)
+                br.wo = INTEG == NORI_INTEGRATOR_DIRECT ? dv : wi;
+                const V3 f = bsdf_eval(B, br);
+                if (INTEG == NORI_INTEGRATOR_DIRECT_MIS) {
+                    const float pdf_mat = bsdf_pdf(B, br);
+                    const float w_em = pdf_mat + ne.pdf_em > 0.f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
+                    color = color + ((f * w_em) * ne.Li) * wi.z;
+                } else {
+                    color = color + (f * wi.z) * ne.Li;
+                }
+            }
+        }
+        if (INTEG == NORI_INTEGRATOR_DIRECT_MATS || INTEG == NORI_INTEGRATOR_DIRECT_MIS) {
+            BRec br;
+            br.wi = to_local(hs.sh, -d);
+            br.wo = V3{0, 0, 1};
+            br.measure = kMeasureUnknown;
+            br.uv = hs.uv;
+            const V3 w = bsdf_sample(B, br, next2D(rng));
+            if (is_zero(w)) return color;  // deviation D1: no ray along an unset direction
+            const float pdf_mat = INTEG == NORI_INTEGRATOR_DIRECT_MIS ? bsdf_pdf(B, br) : 0.0f;
+            SurfHit nh;
+            if (!closest(hs.p, to_world(hs.sh, br.wo), kEps, INF_F, nh)) return color;
+            const DevShape &ns = S.shapes[nh.shape];
+            if (ns.emitter < 0) return color;
+            const DevEmitter &E = S.emitters[ns.emitter];
+            const V3 wl = normalize(nh.p - hs.p);
+            const V3 Le = emitter_eval(S, E, nh.sh.n, wl);
+            if (INTEG == NORI_INTEGRATOR_DIRECT_MATS) return color + w * Le;
+            const float pdf_em = emitter_pdf(S, E, nh.sh.n, wl);
+            const float w_mat = pdf_mat + pdf_em > 0.f ? pdf_mat / (pdf_mat + pdf_em) : 0.0f;
+            return color + (w * w_mat) * Le;
+        }
+        return color;
+    }
+};
+
+template <int STACK, int INTEG>
+__global__ __launch_bounds__(kTraceBlock) void k_direct(DevScene S, WorkDesc wd, float4 *rec, Counters *C) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
+    const uint64_t w = (uint64_t)blockIdx.x * kTraceBlock + threadIdx.x;
+    OneBounce<STACK> ob{S, stk + threadIdx.x};
+    if (w < wd.total) {
+        const uint32_t pass = (uint32_t)(w / wd.M), e = (uint32_t)(w - (uint64_t)pass * wd.M), pix = wd.pixels[e];
+        const uint32_t y = pix / (uint32_t)S.W, x = pix - y * (uint32_t)S.W;
+        Pcg rng;
+        wave_seed(rng, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
+        const V2 jit = next2D(rng);
+        const V2 ap = next2D(rng);  // apertureSample (render.cpp:99)
+        const float px = (float)x + jit.x, py = (float)y + jit.y;
+        V3 L;
+        if (S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f) {
+            // render.cpp:106-121: one ray per colour channel, Li calls in turn,
+            // each weighted by its channel's unit colour
+            V3 o[3], d[3];
+            float mn[3], mx[3];
+            for (int ch = 0; ch < 3; ++ch) camera_sample(S, px, py, ap, ch, o[ch], d[ch], mn[ch], mx[ch]);
+            V3 v[3];
+            for (int ch = 0; ch < 3; ++ch) {
+                const V3 l = ob.template Li<INTEG>(rng, o[ch], d[ch], mn[ch], mx[ch]);
+                v[ch] = V3{ch == 0 ? 1.f : 0.f, ch == 1 ? 1.f : 0.f, ch == 2 ? 1.f : 0.f} * l;
+            }
+            L = (v[0] + v[1]) + v[2];
+        } else {
+            V3 o, d;
+            float mn, mx;
+            camera_sample(S, px, py, ap, -1, o, d, mn, mx);
+            L = V3{1, 1, 1} * ob.template Li<INTEG>(rng, o, d, mn, mx);
+        }
+        rec[w] = make_float4(L.x, L.y, L.z, 0.0f);
+    }
+    // ray counts: one atomic per wave
+    uint32_t rc = ob.rc, rs = ob.rs;
+    for (int off = 32; off > 0; off >>= 1) {
+        rc += __shfl_xor(rc, off);
+        rs += __shfl_xor(rs, off);
+    }
+    if (lane_id() == 0 && (rc | rs)) {
+        atomicAdd(&C->direct_rays[0], (unsigned long long)rc);
+        atomicAdd(&C->direct_rays[1], (unsigned long long)rs);
+    }
+}
+
 // ------------------------------------------------------------------ film splat
 // ImageBlock::put(pos, val) (block.cpp:93-122) for every sample of one 32x32
 // block and a range of passes, then ImageBlock::put(block) (block.cpp:124-133)
@@ -1688,6 +1939,31 @@ hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &
         finish_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else
         finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    return hipGetLastError();
+}
+
+template <int INTEG>
+static void direct_dispatch(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack,
+                            hipStream_t st) {
+    const dim3 g((uint32_t)((wd.total + kTraceBlock - 1) / kTraceBlock)), b(kTraceBlock);
+    switch (stack) {
+    case 0: hipLaunchKernelGGL((k_direct<0, INTEG>), g, b, 0, st, S, wd, rec, C); break;
+    case 8: hipLaunchKernelGGL((k_direct<8, INTEG>), g, b, 0, st, S, wd, rec, C); break;
+    case 16: hipLaunchKernelGGL((k_direct<16, INTEG>), g, b, 0, st, S, wd, rec, C); break;
+    default: hipLaunchKernelGGL((k_direct<32, INTEG>), g, b, 0, st, S, wd, rec, C); break;
+    }
+}
+hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack, hipStream_t st) {
+    if (wd.total == 0) return hipSuccess;
+    switch (S.integrator) {
+    case NORI_INTEGRATOR_NORMALS: direct_dispatch<NORI_INTEGRATOR_NORMALS>(S, wd, rec, C, stack, st); break;
+    case NORI_INTEGRATOR_AV: direct_dispatch<NORI_INTEGRATOR_AV>(S, wd, rec, C, stack, st); break;
+    case NORI_INTEGRATOR_DIRECT: direct_dispatch<NORI_INTEGRATOR_DIRECT>(S, wd, rec, C, stack, st); break;
+    case NORI_INTEGRATOR_DIRECT_EMS: direct_dispatch<NORI_INTEGRATOR_DIRECT_EMS>(S, wd, rec, C, stack, st); break;
+    case NORI_INTEGRATOR_DIRECT_MATS: direct_dispatch<NORI_INTEGRATOR_DIRECT_MATS>(S, wd, rec, C, stack, st); break;
+    case NORI_INTEGRATOR_DIRECT_MIS: direct_dispatch<NORI_INTEGRATOR_DIRECT_MIS>(S, wd, rec, C, stack, st); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -284,6 +284,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         ds.bsdf = sd.bsdf;
         ds.emitter = sd.emitter;
         ds.has_normals = sd.has_normals;
+        ds.has_uvs = sd.has_uvs && d.uvs ? 1u : 0u;
         ds.prim_offset = off;
         for (int k = 0; k < 3; ++k) ds.center[k] = sd.center[k];
         ds.radius = sd.radius;
@@ -357,25 +358,42 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         o.spec_tint = b.specular_tint;
         double r2 = (double)b.roughness * (double)b.roughness;  // disney.cpp:59
         o.d_alpha = (float)(r2 > 1e-3 ? r2 : 1e-3);
+        o.tex = b.albedo_texture;
+        for (int k = 0; k < 3; ++k) o.tex_v2[k] = b.tex_value2[k];
+        for (int k = 0; k < 2; ++k) o.tex_delta[k] = b.tex_delta[k], o.tex_scale[k] = b.tex_scale[k];
+        if (b.albedo_texture != NORI_TEXTURE_CONSTANT && b.albedo_texture != NORI_TEXTURE_CHECKERBOARD)
+            throw NoriException(NORI_ERR_INVALID, "unknown albedo texture");
         if (b.type < NORI_BSDF_DIFFUSE || b.type > NORI_BSDF_DISNEY) throw NoriException(NORI_ERR_INVALID, "unknown bsdf type");
     }
     std::vector<DevEmitter> emitters(d.num_emitters);
     std::vector<float> env;  // envmap tables of every envmap emitter
     for (uint32_t i = 0; i < d.num_emitters; ++i) {
         const nori_emitter_desc &e = d.emitters[i];
-        if (e.type != NORI_EMITTER_AREA && e.type != NORI_EMITTER_ENVMAP)
+        if (e.type != NORI_EMITTER_AREA && e.type != NORI_EMITTER_ENVMAP && e.type != NORI_EMITTER_POINT &&
+            e.type != NORI_EMITTER_SPOT)
             throw NoriException(NORI_ERR_UNSUPPORTED, "unknown emitter type");
-        if (e.shape < 0 || (uint32_t)e.shape >= d.num_shapes) throw NoriException(NORI_ERR_INVALID, "emitter without a shape");
+        const bool free_standing = e.type == NORI_EMITTER_POINT || e.type == NORI_EMITTER_SPOT;
+        if (!free_standing && (e.shape < 0 || (uint32_t)e.shape >= d.num_shapes))
+            throw NoriException(NORI_ERR_INVALID, "emitter without a shape");
         std::memset(&emitters[i], 0, sizeof(DevEmitter));
         emitters[i].type = e.type;
-        emitters[i].shape = e.shape;
-        for (int k = 0; k < 3; ++k) emitters[i].radiance[k] = e.radiance[k];
+        emitters[i].shape = free_standing ? -1 : e.shape;
+        for (int k = 0; k < 3; ++k) {
+            emitters[i].radiance[k] = e.radiance[k];
+            emitters[i].position[k] = e.position[k];
+            emitters[i].power[k] = e.power[k];
+            emitters[i].direction[k] = e.direction[k];
+        }
+        emitters[i].cos_fs = e.cos_falloff_start;
+        emitters[i].cos_tw = e.cos_total_width;
         if (e.type == NORI_EMITTER_ENVMAP) build_envmap(e, emitters[i], env);
     }
-    if (d.num_emitters == 0) throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
-    if (d.integrator != NORI_INTEGRATOR_PATH_MIS && d.integrator != NORI_INTEGRATOR_PATH_MATS &&
-        d.integrator != NORI_INTEGRATOR_VOLUMETRIC)
+    if (d.integrator < NORI_INTEGRATOR_PATH_MATS || d.integrator > NORI_INTEGRATOR_DIRECT_MIS)
         throw NoriException(NORI_ERR_UNSUPPORTED, "unknown integrator");
+    if (d.num_emitters == 0 && d.integrator != NORI_INTEGRATOR_NORMALS && d.integrator != NORI_INTEGRATOR_AV)
+        throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
+    if (d.camera.camera_type < NORI_CAMERA_PERSPECTIVE || d.camera.camera_type > NORI_CAMERA_ADVANCED)
+        throw NoriException(NORI_ERR_UNSUPPORTED, "unknown camera type");
     // the reference leaves Scene::m_medium uninitialised without a <medium>
     // (scene.h:141): rejected here, as in the oracle
     if (d.integrator == NORI_INTEGRATOR_VOLUMETRIC && !d.medium.present)
@@ -435,11 +453,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     const std::vector<float> &prim_list = scan ? scan_prims : bvh.prims;
 
     std::vector<float> pos(4 * (size_t)d.num_vertices), nrm(4 * (size_t)d.num_vertices);
-    for (uint32_t v = 0; v < d.num_vertices; ++v)
+    for (uint32_t v = 0; v < d.num_vertices; ++v) {
         for (int k = 0; k < 3; ++k) {
             pos[4 * (size_t)v + k] = d.positions[3 * (size_t)v + k];
             nrm[4 * (size_t)v + k] = d.normals ? d.normals[3 * (size_t)v + k] : 0.0f;
         }
+        // texture coordinates ride in the w lanes (u with the position, v with the normal)
+        pos[4 * (size_t)v + 3] = d.uvs ? d.uvs[2 * (size_t)v] : 0.0f;
+        nrm[4 * (size_t)v + 3] = d.uvs ? d.uvs[2 * (size_t)v + 1] : 0.0f;
+    }
     if (pos.empty()) pos.assign(4, 0.0f), nrm.assign(4, 0.0f);
     if (cdf.empty()) cdf.assign(1, 0.0f);
     c.nodes.upload(bvh.nodes);
@@ -525,6 +547,14 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     }
     S.near_clip = cam.near_clip;
     S.far_clip = cam.far_clip;
+    S.cam_type = cam.camera_type;
+    S.lens_radius = cam.lens_radius;
+    S.focal = cam.focal_distance;
+    S.distortion[0] = cam.distortion[0];
+    S.distortion[1] = cam.distortion[1];
+    for (int k = 0; k < 3; ++k) S.chromatic[k] = cam.camera_type == NORI_CAMERA_ADVANCED ? cam.chromatic[k] : 0.0f;
+    S.W_max = cam.width > cam.height ? cam.width : cam.height;
+    S.av_length = d.av_length;
     filter_table(cam, S.filter);
     S.filter_radius = cam.filter_radius;
     S.lookup = NORI_FILTER_RESOLUTION / cam.filter_radius;
@@ -613,6 +643,100 @@ bool overlap_splat() {
     return !(e && e[0] == '0');
 }
 
+// normals / av / direct*: no path pool -- per chunk of passes, k_direct runs
+// every sample start to end and writes its record, then k_splat filters them.
+int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std::vector<uint32_t> &pixels,
+                      const std::vector<int4> &blocks, float *rgbw_out, nori_gpu_stats *stats,
+                      std::chrono::steady_clock::time_point t0) {
+    const DevScene &S = c.S;
+    const int W = S.W, H = S.H, B = S.border;
+    const uint32_t M = (uint32_t)pixels.size(), passes = rd.pass_count;
+    const size_t rec_budget = (size_t)4 << 30;
+    uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(passes, rec_budget / (16 * (size_t)M)));
+    chunk = (uint32_t)std::min<uint64_t>(chunk, ((uint64_t)1 << 31) / M);
+    c.rec.ensure(16 * (size_t)chunk * M);
+    c.counters.ensure(sizeof(Counters));
+    c.pixels.upload(pixels);
+    c.blocks.upload(blocks);
+    const size_t film_elems = 4 * (size_t)(W + 2 * B) * (H + 2 * B);
+    float *film = nullptr;
+    if (rd.output_on_device) {
+        film = rgbw_out;
+    } else {
+        c.film.ensure(film_elems * sizeof(float));
+        film = c.film.as<float>();
+        HIP_TRY(hipMemsetAsync(film, 0, film_elems * sizeof(float), c.stream));
+    }
+    Counters *C = c.counters.as<Counters>();
+    HIP_TRY(hipMemsetAsync(C, 0, sizeof(Counters), c.stream));
+    c.cancel = 0;
+    c.progress = 0.0f;
+    Timers tm;
+    const bool timing = rd.timing != 0;
+    double kms[2] = {0, 0};
+    std::vector<std::array<hipEvent_t, 3>> spans;
+    uint64_t done = 0;
+    bool cancelled = false;
+    for (uint32_t p0 = 0; p0 < passes; p0 += chunk) {
+        if (c.cancel.load()) {
+            cancelled = true;
+            break;
+        }
+        const uint32_t np = std::min(chunk, passes - p0);
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, 0, nullptr, 1, 0};
+        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)), c.blocks.as<int4>(),
+                     rd.seed};
+        std::array<hipEvent_t, 3> ev{};
+        if (timing) {
+            for (auto &e : ev) e = tm.get();
+            HIP_TRY(hipEventRecord(ev[0], c.stream));
+        }
+        HIP_TRY(launch_direct(S, wd, c.rec.as<float4>(), C, c.stack, c.stream));
+        if (timing) HIP_TRY(hipEventRecord(ev[1], c.stream));
+        HIP_TRY(launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, c.stream));
+        if (timing) {
+            HIP_TRY(hipEventRecord(ev[2], c.stream));
+            spans.push_back(ev);
+        }
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        done += wd.total;
+        c.progress = (float)((double)(p0 + np) / passes);
+    }
+    Counters hc;
+    HIP_TRY(hipMemcpyAsync(&hc, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    for (const auto &e : spans) {
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
+        kms[0] += a;
+        kms[1] += b;
+    }
+    if (!rd.output_on_device && !cancelled) {
+        std::vector<float> hf(film_elems);
+        HIP_TRY(hipMemcpy(hf.data(), film, film_elems * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < film_elems; ++i) rgbw_out[i] += hf[i];
+    }
+    c.progress = 1.0f;
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->samples = done;
+        stats->invalid_samples = hc.invalid;
+        stats->rays_closest = hc.direct_rays[0];
+        stats->rays_shadow = hc.direct_rays[1];
+        stats->iterations = 0;
+        stats->scene_bytes = c.scene_bytes;
+        stats->bvh_nodes = c.bvh_nodes;
+        stats->bvh_depth = c.bvh_depth;
+        stats->stream_parts = 1;
+        stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->ms_shade = kms[0];  // k_direct: the whole integrator
+        stats->ms_splat = kms[1];
+    }
+    if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
+    return NORI_OK;
+}
+
 int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nori_gpu_stats *stats) {
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(c.device));
@@ -645,8 +769,13 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     const uint32_t M = (uint32_t)pixels.size();
     const uint32_t passes = rd.pass_count ? rd.pass_count : 0;
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
+    const bool one_bounce = S.integrator >= NORI_INTEGRATOR_NORMALS;
+    if (!one_bounce && (S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f))
+        throw NoriException(NORI_ERR_UNSUPPORTED,
+                            "chromatic aberration (three rays per sample) is on the one-bounce integrators only");
     // default pool: 4M paths in flight (~0.9 GB of queues); measured best among
     // 256K..4M on cbox (larger pools hide the shade kernel's memory latency)
+    if (one_bounce) return render_one_bounce(c, rd, pixels, blocks, rgbw_out, stats, t0);
     uint32_t pool = rd.path_pool;
     if (!pool) {  // NORI_PATH_POOL: default pool size override (tuning)
         const char *e = std::getenv("NORI_PATH_POOL");

@@ -9,9 +9,8 @@
 //     ctor(props) -> addChild -> setParent -> activate (parser.cpp:28-338);
 //   * WavefrontOBJ loading with quad split and vertex de-duplication
 //     (obj.cpp:32-132).
-// Integrators, cameras, samplers and media outside this path's scope (direct*,
-// normals, av, photonmapper, thinlens, advanced camera, point/spot lights,
-// textures other than constant_*) are rejected with NORI_ERR_UNSUPPORTED.
+// Plugins outside this path's scope (photonmapper, image textures, normal
+// maps, Perlin noise) are rejected with NORI_ERR_UNSUPPORTED.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -309,6 +308,17 @@ class PropertyList {  // proplist.cpp:23-61
     Vec3f getPoint3(const std::string &n, Vec3f d) const { auto p = get(n, Property::Point3); return p ? p->v : d; }
     Vec3f getVector3(const std::string &n, Vec3f d) const { auto p = get(n, Property::Vector3); return p ? p->v : d; }
     Vec3f getVector3(const std::string &n) const { return req(n, Property::Vector3).v; }
+    Vec3f getPoint3(const std::string &n) const { return req(n, Property::Point3).v; }
+    void getPoint2(const std::string &n, float out[2], float d0, float d1) const {
+        auto p = get(n, Property::Point2);
+        out[0] = p ? p->v2[0] : d0;
+        out[1] = p ? p->v2[1] : d1;
+    }
+    void getVector2(const std::string &n, float out[2], float d0, float d1) const {
+        auto p = get(n, Property::Vector2);
+        out[0] = p ? p->v2[0] : d0;
+        out[1] = p ? p->v2[1] : d1;
+    }
     Mat4 getTransform(const std::string &n, const Mat4 &d) const { auto p = get(n, Property::Transform); return p ? p->t : d; }
 
   private:
@@ -352,9 +362,8 @@ struct Registrar {
 struct Unsupported : NoriObject {
     EClassType getClassType() const override { return EClassTypeCount; }
 };
-static const char *kUnsupported[] = {"direct", "direct_ems", "direct_mats", "direct_mis", "normals", "av",
-                                     "photonmapper", "thinlens", "advancedCamera", "point", "spotlight",
-                                     "checkerboard", "image_texture", "normal_map", "perlin", "chi2test"};
+static const char *kUnsupported[] = {"photonmapper", "checkerboard_float", "image_texture", "normal_map", "perlin",
+                                     "chi2test"};
 
 // ---- textures (consttexture.cpp)
 struct ConstantColor : NoriObject {
@@ -369,10 +378,24 @@ struct ConstantFloat : NoriObject {
     EClassType getClassType() const override { return ETexture; }
 };
 NORI_REGISTER_CLASS(ConstantFloat, "constant_float")
+struct CheckerboardColor : NoriObject {  // checkerboard.cpp:62-68 (Checkerboard<Color3f>)
+    Vec3f value1, value2;
+    float delta[2], scale[2];
+    explicit CheckerboardColor(const PropertyList &p)
+        : value1(p.getColor("value1", Vec3f{0, 0, 0})), value2(p.getColor("value2", Vec3f{1, 1, 1})) {
+        p.getPoint2("delta", delta, 0.f, 0.f);
+        p.getVector2("scale", scale, 1.f, 1.f);
+    }
+    EClassType getClassType() const override { return ETexture; }
+};
+NORI_REGISTER_CLASS(CheckerboardColor, "checkerboard_color")
 
 // ---- BSDFs
 struct Bsdf : NoriObject {
     nori_bsdf_desc d{};
+    // consumed children (textures) stay alive until the BSDF dies: the parser
+    // calls setParent on a child after addChild (parser.cpp:208-211)
+    std::vector<std::unique_ptr<NoriObject>> consumed;
     EClassType getClassType() const override { return EBSDF; }
 };
 struct Diffuse : Bsdf {  // diffuse.cpp:29-66
@@ -390,11 +413,19 @@ struct Diffuse : Bsdf {  // diffuse.cpp:29-66
             throw NoriException(NORI_ERR_PARSE, std::string("Diffuse::addChild(<") + class_name(o->getClassType()) + ">) is not supported!");
         if (o->idName != "albedo") throw NoriException(NORI_ERR_PARSE, "The name of this texture does not match any field!");
         if (has_albedo) throw NoriException(NORI_ERR_PARSE, "There is already an albedo defined!");
-        auto *c = dynamic_cast<ConstantColor *>(o);
-        if (!c) throw NoriException(NORI_ERR_UNSUPPORTED, "only constant_color albedo textures are on this path");
-        d.albedo[0] = c->value.x; d.albedo[1] = c->value.y; d.albedo[2] = c->value.z;
+        if (auto *c = dynamic_cast<ConstantColor *>(o)) {
+            d.albedo[0] = c->value.x; d.albedo[1] = c->value.y; d.albedo[2] = c->value.z;
+        } else if (auto *k = dynamic_cast<CheckerboardColor *>(o)) {
+            d.albedo_texture = NORI_TEXTURE_CHECKERBOARD;
+            d.albedo[0] = k->value1.x; d.albedo[1] = k->value1.y; d.albedo[2] = k->value1.z;
+            d.tex_value2[0] = k->value2.x; d.tex_value2[1] = k->value2.y; d.tex_value2[2] = k->value2.z;
+            d.tex_delta[0] = k->delta[0]; d.tex_delta[1] = k->delta[1];
+            d.tex_scale[0] = k->scale[0]; d.tex_scale[1] = k->scale[1];
+        } else {
+            throw NoriException(NORI_ERR_UNSUPPORTED, "albedo textures: constant_color and checkerboard_color are on this path");
+        }
         has_albedo = true;
-        delete o;
+        consumed.emplace_back(o);
     }
     void activate() override {
         if (!has_albedo) { d.albedo[0] = d.albedo[1] = d.albedo[2] = 0.5f; has_albedo = true; }
@@ -436,7 +467,7 @@ struct Disney : Bsdf {  // disney.cpp:46-60
         Vec3f b = p.getColor("baseColor", Vec3f{0, 0, 0});
         d.base_color[0] = b.x; d.base_color[1] = b.y; d.base_color[2] = b.z;
     }
-    void addChild(NoriObject *o) override { delete o; }  // disney.cpp:176: ignores children
+    void addChild(NoriObject *o) override { consumed.emplace_back(o); }  // disney.cpp:176: ignores children
 };
 NORI_REGISTER_CLASS(Disney, "disney")
 
@@ -473,6 +504,30 @@ struct EnvMapEmitter : Emitter {  // envmap.cpp:13-58
     }
 };
 NORI_REGISTER_CLASS(EnvMapEmitter, "envmap")
+struct PointEmitter : Emitter {  // pointlight.cpp:11-15
+    explicit PointEmitter(const PropertyList &p) {
+        d.type = NORI_EMITTER_POINT;
+        d.shape = -1;
+        Vec3f q = p.getPoint3("position", Vec3f{0, 0, 0}), w = p.getColor("power", Vec3f{0, 0, 0});
+        d.position[0] = q.x; d.position[1] = q.y; d.position[2] = q.z;
+        d.power[0] = w.x; d.power[1] = w.y; d.power[2] = w.z;
+    }
+};
+NORI_REGISTER_CLASS(PointEmitter, "point")
+struct SpotEmitter : Emitter {  // spotlight.cpp:11-18
+    explicit SpotEmitter(const PropertyList &p) {
+        d.type = NORI_EMITTER_SPOT;
+        d.shape = -1;
+        Vec3f q = p.getPoint3("position"), c = p.getColor("color"), dir = normalized(p.getVector3("direction"));
+        d.position[0] = q.x; d.position[1] = q.y; d.position[2] = q.z;
+        d.power[0] = c.x; d.power[1] = c.y; d.power[2] = c.z;
+        d.direction[0] = dir.x; d.direction[1] = dir.y; d.direction[2] = dir.z;
+        // std::cos(M_PI / 180 * deg): M_PI is a float literal (common.h:56), the cos is the float overload
+        d.cos_falloff_start = std::cos(3.14159265358979323846f / 180 * p.getFloat("falloffStart"));
+        d.cos_total_width = std::cos(3.14159265358979323846f / 180 * p.getFloat("totalWidth"));
+    }
+};
+NORI_REGISTER_CLASS(SpotEmitter, "spotlight")
 
 // ---- shapes
 struct Shape : NoriObject {
@@ -658,7 +713,8 @@ NORI_REGISTER_CLASS(Windowed, "windowed")
 struct Perspective : NoriObject {
     nori_camera_desc d{};
     RFilter *filter = nullptr;
-    explicit Perspective(const PropertyList &p) {
+    explicit Perspective(const PropertyList &p, int type = NORI_CAMERA_PERSPECTIVE) {
+        d.camera_type = type;
         d.width = p.getInteger("width", 1280);
         d.height = p.getInteger("height", 720);
         Mat4 c2w = p.getTransform("toWorld", mat_identity());
@@ -683,6 +739,23 @@ struct Perspective : NoriObject {
     }
 };
 NORI_REGISTER_CLASS(Perspective, "perspective")
+struct ThinLens : Perspective {  // thinlens.cpp:30-51
+    explicit ThinLens(const PropertyList &p) : Perspective(p, NORI_CAMERA_THINLENS) {
+        d.focal_distance = p.getFloat("focalDist", 1.0f);
+        d.lens_radius = p.getFloat("lensRadius", 0.0f);
+    }
+};
+NORI_REGISTER_CLASS(ThinLens, "thinlens")
+struct AdvancedCam : Perspective {  // advancedCamera.cpp:30-55
+    explicit AdvancedCam(const PropertyList &p) : Perspective(p, NORI_CAMERA_ADVANCED) {
+        d.focal_distance = p.getFloat("focalDist", 1.0f);
+        d.lens_radius = p.getFloat("lensRadius", 0.0f);
+        p.getVector2("distortion", d.distortion, 0.f, 0.f);
+        Vec3f c = p.getVector3("chromaticAberation", Vec3f{0, 0, 0});
+        d.chromatic[0] = c.x; d.chromatic[1] = c.y; d.chromatic[2] = c.z;
+    }
+};
+NORI_REGISTER_CLASS(AdvancedCam, "advancedCamera")
 
 // perspective.cpp:53-82, evaluated for the (possibly overridden) output size.
 void compute_sample_to_camera(nori_camera_desc &d) {
@@ -720,6 +793,21 @@ struct PathMis : Integrator { explicit PathMis(const PropertyList &) : Integrato
 NORI_REGISTER_CLASS(PathMis, "path_mis")
 struct Volumetric : Integrator { explicit Volumetric(const PropertyList &) : Integrator(NORI_INTEGRATOR_VOLUMETRIC) {} };
 NORI_REGISTER_CLASS(Volumetric, "volumetric")
+struct Normals : Integrator { explicit Normals(const PropertyList &) : Integrator(NORI_INTEGRATOR_NORMALS) {} };
+NORI_REGISTER_CLASS(Normals, "normals")
+struct AverageVisibility : Integrator {  // averagevisibility.cpp:11-14
+    float length;
+    explicit AverageVisibility(const PropertyList &p) : Integrator(NORI_INTEGRATOR_AV), length(p.getFloat("length")) {}
+};
+NORI_REGISTER_CLASS(AverageVisibility, "av")
+struct Direct : Integrator { explicit Direct(const PropertyList &) : Integrator(NORI_INTEGRATOR_DIRECT) {} };
+NORI_REGISTER_CLASS(Direct, "direct")
+struct DirectEms : Integrator { explicit DirectEms(const PropertyList &) : Integrator(NORI_INTEGRATOR_DIRECT_EMS) {} };
+NORI_REGISTER_CLASS(DirectEms, "direct_ems")
+struct DirectMats : Integrator { explicit DirectMats(const PropertyList &) : Integrator(NORI_INTEGRATOR_DIRECT_MATS) {} };
+NORI_REGISTER_CLASS(DirectMats, "direct_mats")
+struct DirectMis : Integrator { explicit DirectMis(const PropertyList &) : Integrator(NORI_INTEGRATOR_DIRECT_MIS) {} };
+NORI_REGISTER_CLASS(DirectMis, "direct_mis")
 struct Phase : NoriObject {
     explicit Phase(const PropertyList &) {}
     EClassType getClassType() const override { return EPhaseFunction; }
@@ -752,6 +840,7 @@ NORI_REGISTER_CLASS(Medium, "medium")
 struct SceneObj : NoriObject {
     std::vector<Shape *> shapes;
     std::vector<Emitter *> emitters;  // addChild order (scene.cpp:63-77)
+    std::vector<Emitter *> free_emitters;  // owned here (shape emitters are owned by their shape)
     Independent *sampler = nullptr;
     Perspective *camera = nullptr;
     Integrator *integrator = nullptr;
@@ -759,6 +848,7 @@ struct SceneObj : NoriObject {
     explicit SceneObj(const PropertyList &) {}
     ~SceneObj() override {
         for (auto *s : shapes) { if (s->emitter) { delete s->emitter; s->emitter = nullptr; } delete s; }
+        for (auto *e : free_emitters) delete e;
         delete sampler; delete camera; delete integrator; delete medium;
     }
     EClassType getClassType() const override { return EScene; }
@@ -770,8 +860,10 @@ struct SceneObj : NoriObject {
             if (m->emitter) emitters.push_back(m->emitter);
             break;
         }
-        case EEmitter:
-            throw NoriException(NORI_ERR_UNSUPPORTED, "free-standing emitters (point/spot) are not on this path");
+        case EEmitter:  // free-standing emitters (scene.cpp:73-75)
+            emitters.push_back(static_cast<Emitter *>(o));
+            free_emitters.push_back(static_cast<Emitter *>(o));
+            break;
         case ESampler:
             if (sampler) throw NoriException(NORI_ERR_PARSE, "There can only be one sampler per scene!");
             sampler = static_cast<Independent *>(o);
@@ -1021,7 +1113,12 @@ HostScene *load_scene_xml(const std::string &path, int width, int height, int sp
             }
         hs->emitters.push_back(ed);
     }
-    if (hs->emitters.empty()) throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
+    const int integ = sc->integrator->kind;
+    // normals and av never query emitters; every other integrator samples one
+    // (Scene::getRandomEmitter on an empty list is undefined, scene.h:68-74)
+    if (hs->emitters.empty() && integ != NORI_INTEGRATOR_NORMALS && integ != NORI_INTEGRATOR_AV)
+        throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
+    if (integ == NORI_INTEGRATOR_AV) hs->desc.av_length = static_cast<AverageVisibility *>(sc->integrator)->length;
     nori_camera_desc cam = sc->camera->d;
     if (width > 0) cam.width = width;
     if (height > 0) cam.height = height;

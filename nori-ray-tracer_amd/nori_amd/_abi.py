@@ -1,4 +1,4 @@
-"""ctypes mirror of include/nori_gpu.h (ABI version 1).
+"""ctypes mirror of include/nori_gpu.h (ABI version 2).
 
 The structures below must match the C declarations field for field; the
 test suite checks their sizes against the library (tests/test_abi.py).
@@ -6,7 +6,7 @@ test suite checks their sizes against the library (tests/test_abi.py).
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 NORI_OK = 0
 NORI_ERR_INVALID = -1
@@ -19,9 +19,13 @@ NORI_ERR_OOM = -7
 
 SHAPE_MESH, SHAPE_SPHERE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET, BSDF_DISNEY = range(5)
-EMITTER_AREA, EMITTER_ENVMAP = 0, 1
-INTEGRATOR_PATH_MATS, INTEGRATOR_PATH_MIS, INTEGRATOR_VOLUMETRIC = 0, 1, 2
-INTEGRATOR_NAMES = {0: "path_mats", 1: "path_mis", 2: "volumetric"}
+EMITTER_AREA, EMITTER_ENVMAP, EMITTER_POINT, EMITTER_SPOT = 0, 1, 2, 3
+TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD = 0, 1
+CAMERA_PERSPECTIVE, CAMERA_THINLENS, CAMERA_ADVANCED = 0, 1, 2
+(INTEGRATOR_PATH_MATS, INTEGRATOR_PATH_MIS, INTEGRATOR_VOLUMETRIC, INTEGRATOR_NORMALS, INTEGRATOR_AV,
+ INTEGRATOR_DIRECT, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS) = range(9)
+INTEGRATOR_NAMES = {0: "path_mats", 1: "path_mis", 2: "volumetric", 3: "normals", 4: "av", 5: "direct",
+                    6: "direct_ems", 7: "direct_mats", 8: "direct_mis"}
 RNG_WAVE, RNG_BLOCK = 0, 1
 BLOCK_SIZE = 32
 FILTER_RESOLUTION = 32
@@ -39,13 +43,16 @@ class BsdfDesc(C.Structure):
                 ("ext_ior", C.c_float), ("alpha", C.c_float), ("kd", C.c_float * 3),
                 ("base_color", C.c_float * 3), ("metallic", C.c_float), ("specular", C.c_float),
                 ("roughness", C.c_float), ("sheen", C.c_float), ("sheen_tint", C.c_float),
-                ("specular_tint", C.c_float)]
+                ("specular_tint", C.c_float), ("albedo_texture", C.c_int32), ("tex_value2", C.c_float * 3),
+                ("tex_delta", C.c_float * 2), ("tex_scale", C.c_float * 2)]
 
 
 class EmitterDesc(C.Structure):
     _fields_ = [("type", C.c_int32), ("shape", C.c_int32), ("radiance", C.c_float * 3),
                 ("weight", C.c_float), ("lum_scale", C.c_float * 3), ("env_rows", C.c_int32),
-                ("env_cols", C.c_int32), ("env_rgb", C.POINTER(C.c_float))]
+                ("env_cols", C.c_int32), ("env_rgb", C.POINTER(C.c_float)),
+                ("position", C.c_float * 3), ("power", C.c_float * 3), ("direction", C.c_float * 3),
+                ("cos_falloff_start", C.c_float), ("cos_total_width", C.c_float)]
 
 
 class CameraDesc(C.Structure):
@@ -53,7 +60,9 @@ class CameraDesc(C.Structure):
                 ("near_clip", C.c_float), ("far_clip", C.c_float),
                 ("camera_to_world", C.c_float * 16), ("sample_to_camera", C.c_float * 16),
                 ("filter_type", C.c_int32), ("filter_radius", C.c_float),
-                ("filter_p0", C.c_float), ("filter_p1", C.c_float)]
+                ("filter_p0", C.c_float), ("filter_p1", C.c_float),
+                ("camera_type", C.c_int32), ("lens_radius", C.c_float), ("focal_distance", C.c_float),
+                ("distortion", C.c_float * 2), ("chromatic", C.c_float * 3)]
 
 
 class MediumDesc(C.Structure):
@@ -69,7 +78,8 @@ class SceneDesc(C.Structure):
                 ("shapes", C.POINTER(ShapeDesc)), ("num_bsdfs", C.c_uint32),
                 ("bsdfs", C.POINTER(BsdfDesc)), ("num_emitters", C.c_uint32),
                 ("emitters", C.POINTER(EmitterDesc)), ("camera", CameraDesc),
-                ("medium", MediumDesc), ("integrator", C.c_int32), ("sample_count", C.c_uint32)]
+                ("medium", MediumDesc), ("integrator", C.c_int32), ("sample_count", C.c_uint32),
+                ("av_length", C.c_float)]
 
 
 class RenderDesc(C.Structure):

@@ -217,7 +217,7 @@ static inline float sq_gtr2_pdf(V3 m, float alpha) {
 
 /* ------------------------------------------------------------------ BSDFs */
 enum { M_UNKNOWN = 0, M_SOLID_ANGLE = 1, M_DISCRETE = 2 }; /* common.h:199-203 */
-typedef struct { V3 wi, wo; float eta; int measure; } BRec;
+typedef struct { V3 wi, wo; float eta; int measure; V2 uv; } BRec;  /* bsdf.h:33-56 */
 
 typedef struct {
     int type;
@@ -226,6 +226,8 @@ typedef struct {
     V3 kd;
     /* disney */
     V3 base; float metallic, specular, roughness, sheen, sheen_tint, spec_tint, d_alpha;
+    /* diffuse albedo texture: constant (albedo) or checkerboard (albedo = value1) */
+    int tex; V3 tex_v2; float tex_delta[2], tex_scale[2];
 } Bsdf;
 
 static void bsdf_init(Bsdf *b, const nori_bsdf_desc *d) {
@@ -242,6 +244,19 @@ static void bsdf_init(Bsdf *b, const nori_bsdf_desc *d) {
         double r2 = (double)d->roughness * (double)d->roughness;
         b->d_alpha = (float)(r2 > 1e-3 ? r2 : 1e-3);
     }
+    b->tex = d->albedo_texture;
+    b->tex_v2 = v3(d->tex_value2[0], d->tex_value2[1], d->tex_value2[2]);
+    b->tex_delta[0] = d->tex_delta[0]; b->tex_delta[1] = d->tex_delta[1];
+    b->tex_scale[0] = d->tex_scale[0]; b->tex_scale[1] = d->tex_scale[1];
+}
+
+/* Texture<Color3f>::eval(uv): ConstantTexture (consttexture.cpp) or
+ * Checkerboard::eval (checkerboard.cpp:22-27) */
+static inline V3 albedo_at(const Bsdf *b, V2 uv) {
+    if (b->tex != NORI_TEXTURE_CHECKERBOARD) return b->albedo;
+    int x = (int)fabsf(floorf(uv.x / b->tex_scale[0] - b->tex_delta[0]));
+    int y = (int)fabsf(floorf(uv.y / b->tex_scale[1] - b->tex_delta[1]));
+    return x % 2 == y % 2 ? b->albedo : b->tex_v2;
 }
 
 /* microfacet.cpp:47-53 */
@@ -277,7 +292,7 @@ static V3 bsdf_eval(const Bsdf *b, const BRec *r) {
     switch (b->type) {
     case NORI_BSDF_DIFFUSE: /* diffuse.cpp:72-82 */
         if (r->measure != M_SOLID_ANGLE || r->wi.z <= 0 || r->wo.z <= 0) return v3(0, 0, 0);
-        return vmuls(b->albedo, F_INV_PI);
+        return vmuls(albedo_at(b, r->uv), F_INV_PI);
     case NORI_BSDF_MICROFACET: { /* microfacet.cpp:79-90 */
         V3 n = vnormalize(vadd(r->wi, r->wo));
         float D = beckmann_D(b, n);
@@ -350,7 +365,7 @@ static V3 bsdf_sample(const Bsdf *b, BRec *r, V2 s) {
         r->measure = M_SOLID_ANGLE;
         r->wo = sq_cosine_hemisphere(s);
         r->eta = 1.0f;
-        return b->albedo;
+        return albedo_at(b, r->uv);
     case NORI_BSDF_MIRROR: /* mirror.cpp:39-55 */
         if (r->wi.z <= 0) return v3(0, 0, 0);
         r->wo = v3(-r->wi.x, -r->wi.y, r->wi.z);
@@ -495,7 +510,7 @@ typedef struct {
     int type;
     uint32_t prim_offset, prim_count;   /* global primitive range */
     uint32_t tri_offset;                /* into scene triangle list */
-    int has_normals;
+    int has_normals, has_uvs;
     V3 center; float radius;
     int bsdf, emitter;
     /* mesh area DiscretePDF (mesh.cpp:30-38, dpdf.h) */
@@ -512,6 +527,8 @@ typedef struct {
     const float *rgb;            /* R*C*3, row-major */
     float *pdf, *cdf;            /* R x C, R x (C+1), row-major */
     float *pmarg, *cmarg;        /* R, R+1 */
+    /* point (pointlight.cpp) / spot (spotlight.cpp) */
+    V3 pos, power, dir; float cos_fs, cos_tw;
 } Emitter;
 
 typedef struct { uint32_t flag_size; uint32_t start_right; BBox bbox; } Node; /* bvh.h:127-164 */
@@ -538,6 +555,9 @@ struct oracle_scene {
     /* medium */
     int has_medium; BBox mbounds; V3 sigma_t, albedo;
     int integrator;
+    float av_length;
+    /* thinlens / advancedCamera */
+    int cam_type; float lens_radius, focal; float distortion[2]; V3 chromatic;
 };
 
 static inline V3 vtx(const oracle_scene *s, uint32_t i) { return v3(s->P[3 * i], s->P[3 * i + 1], s->P[3 * i + 2]); }
@@ -709,6 +729,13 @@ static int bvh_build(oracle_scene *s) {
     return 0;
 }
 
+/* sphericalCoordinates (common.cpp:264-272): (theta, phi), phi in [0, 2pi) */
+static inline V2 spherical_coords(V3 v) {
+    V2 r = {acosf(v.z), atan2f(v.y, v.x)};
+    if (r.y < 0) r.y += 2 * F_PI;
+    return r;
+}
+
 /* ---- intersection (mesh.cpp:83-120, sphere.cpp:43-76, bvh.cpp:404-462) --- */
 typedef struct {
     V3 p; float t; V2 uv; Frame sh, geo; int shape; uint32_t prim; /* global */
@@ -753,6 +780,9 @@ static void set_hit_info(const oracle_scene *s, int si, uint32_t local, const Ra
         its->p = vadd(ray->o, vmuls(ray->d, its->t));
         V3 n = vnormalize(vsub(its->p, sh->center));
         its->sh = frame_from(n); its->geo = its->sh;
+        V2 c = spherical_coords(n);
+        its->uv.x = (float)(0.5 + (double)(c.x / (2 * F_PI)));  /* 0.5 is a double literal */
+        its->uv.y = c.y / F_PI;
         return;
     }
     /* mesh.cpp:122-170 */
@@ -760,6 +790,12 @@ static void set_hit_info(const oracle_scene *s, int si, uint32_t local, const Ra
     V3 p0, p1, p2; uint32_t i0, i1, i2;
     tri_verts(s, sh, local, &p0, &p1, &p2, &i0, &i1, &i2);
     its->p = vadd(vadd(vmuls(p0, bx), vmuls(p1, by)), vmuls(p2, bz));
+    its->uv.x = its->u; its->uv.y = its->v;  /* rayIntersect leaves the barycentrics in its.uv */
+    if (sh->has_uvs) {
+        const float *T = s->desc.uvs;
+        its->uv.x = (bx * T[2 * i0] + by * T[2 * i1]) + bz * T[2 * i2];
+        its->uv.y = (bx * T[2 * i0 + 1] + by * T[2 * i1 + 1]) + bz * T[2 * i2 + 1];
+    }
     its->geo = frame_from(vnormalize(vcross(vsub(p1, p0), vsub(p2, p0))));
     if (sh->has_normals) {
         V3 n = vadd(vadd(vmuls(nrm(s, i0), bx), vmuls(nrm(s, i1), by)), vmuls(nrm(s, i2), bz));
@@ -966,17 +1002,47 @@ static V3 env_sample(const Emitter *e, V2 smp, V3 *wi) {
     return v3(c.x / v_pdf, c.y / v_pdf, c.z / v_pdf);
 }
 
+/* SpotLight::falloff (spotlight.cpp:40-46) */
+static inline float spot_falloff(const Emitter *e, V3 w) {
+    float cosTheta = vdot(e->dir, vnormalize(w));
+    if (cosTheta < e->cos_tw) return 0;
+    if (cosTheta > e->cos_fs) return 1;
+    return (acosf(e->cos_tw) - acosf(cosTheta)) / (acosf(e->cos_tw) - acosf(e->cos_fs));
+}
 static inline V3 emitter_eval(const Emitter *e, const ERec *r) {
     if (e->type == NORI_EMITTER_ENVMAP) return env_eval(e, r->wi);
+    if (e->type == NORI_EMITTER_POINT) { /* pointlight.cpp:27-30 */
+        V3 d = vsub(e->pos, r->ref);
+        return vdivs(e->power, 4.f * F_PI * vdot(d, d));
+    }
+    if (e->type == NORI_EMITTER_SPOT) { /* spotlight.cpp:48-52: a constant (Color3f * scalar takes a float) */
+        V3 c = vdivs(e->power, 4.f * F_PI);
+        float k = (float)(1 - 0.5 * (double)(e->cos_fs + e->cos_tw));
+        return vmuls(vmuls(vmuls(c, 2.0f), F_PI), k);
+    }
     return vdot(r->n, vneg(r->wi)) > 0.0f ? e->radiance : v3(0, 0, 0);
 }
 static inline float emitter_pdf(const oracle_scene *s, const Emitter *e, const ERec *r) {
     if (e->type == NORI_EMITTER_ENVMAP) return env_pdf(e, r->wi);
+    if (e->type == NORI_EMITTER_POINT) return 1.0f;  /* PDF_VALUE, pointlight.cpp:32-35 */
+    if (e->type == NORI_EMITTER_SPOT) return r->pdf; /* spotlight.cpp:54-57 (1 after sample) */
     float theta = vdot(r->n, vneg(r->wi));
     if (theta > 0.0f) return shape_pdf_surface(&s->shapes[e->shape]);
     return 0.0f;
 }
 static V3 emitter_sample(const oracle_scene *s, const Emitter *e, ERec *r, V2 smp) {
+    if (e->type == NORI_EMITTER_POINT || e->type == NORI_EMITTER_SPOT) {
+        /* PointLight::sample (pointlight.cpp:17-25), SpotLight::sample (spotlight.cpp:20-38) */
+        V3 d = vsub(e->pos, r->ref);
+        r->wi = vnormalize(d);
+        r->p = e->pos;
+        r->pdf = 1.0f;
+        r->n = e->dir;
+        r->shadow = ray_make(r->ref, r->wi, EPS, vnorm(d) - EPS);
+        if (e->type == NORI_EMITTER_POINT) return vdivs(e->power, 4.f * F_PI * vdot(d, d));
+        V3 q = vsub(r->ref, r->p);
+        return vdivs(vmuls(e->power, spot_falloff(e, vneg(r->wi))), 4.f * F_PI * vdot(q, q));
+    }
     if (e->type == NORI_EMITTER_ENVMAP) {
         V3 Li = env_sample(e, smp, &r->wi);
         r->shadow = ray_make(r->ref, r->wi, EPS, ENV_T_FAR);
@@ -1046,7 +1112,7 @@ static V3 Li_mats(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c)
         if (next1D(rng) > q) return color;
         att = vdivs(att, q);
         BRec br; memset(&br, 0, sizeof(br));
-        br.wi = to_local(&its.sh, vneg(ray.d));
+        br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv;
         V3 w = bsdf_sample(&s->bsdfs[sh->bsdf], &br, next2D(rng));
         if (vzero(w)) return color;                               /* D1 */
         att = vmul(att, w);
@@ -1077,7 +1143,7 @@ static V3 Li_mis(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c) 
         c->shadow++;
         if (!scene_occluded(s, &er.shadow)) {
             float theta = smax(0.0f, to_local(&its.sh, er.wi).z);
-            BRec br; br.wi = to_local(&its.sh, vneg(ray.d)); br.wo = to_local(&its.sh, er.wi);
+            BRec br; br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv; br.wo = to_local(&its.sh, er.wi);
             br.measure = M_SOLID_ANGLE; br.eta = 1.0f;
             V3 f = bsdf_eval(bsdf, &br);
             float pdf_mat = bsdf_pdf(bsdf, &br);
@@ -1088,7 +1154,7 @@ static V3 Li_mis(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c) 
         if (next1D(rng) > q) return color;
         att = vdivs(att, q);
         BRec br; memset(&br, 0, sizeof(br));
-        br.wi = to_local(&its.sh, vneg(ray.d));
+        br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv;
         V3 w = bsdf_sample(bsdf, &br, next2D(rng));
         if (vzero(w)) return color;                               /* D1 */
         att = vmul(att, w);
@@ -1162,7 +1228,7 @@ static V3 Li_vol(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c) 
             if (!scene_occluded(s, &er.shadow)) {
                 float pdf_em = emitter_pdf(s, light, &er);
                 float theta = smax(0.0f, to_local(&its.sh, er.wi).z);
-                BRec br; br.wi = to_local(&its.sh, vneg(ray.d)); br.wo = to_local(&its.sh, er.wi);
+                BRec br; br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv; br.wo = to_local(&its.sh, er.wi);
                 br.measure = M_SOLID_ANGLE; br.eta = 1.0f;
                 V3 f = bsdf_eval(bsdf, &br);
                 float pdf_mat = bsdf_pdf(bsdf, &br);
@@ -1174,7 +1240,7 @@ static V3 Li_vol(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c) 
             if (next1D(rng) > q) return color;
             att = vdivs(att, q);
             BRec br; memset(&br, 0, sizeof(br));
-            br.wi = to_local(&its.sh, vneg(ray.d));
+            br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv;
             V3 w = bsdf_sample(bsdf, &br, next2D(rng));
             if (vzero(w)) return color;                           /* D1 */
             att = vmul(att, w);
@@ -1198,10 +1264,121 @@ static V3 Li_vol(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c) 
     return color;
 }
 
+/* ---- one-bounce integrators --------------------------------------------- */
+/* normals.cpp:16-24 */
+static V3 Li_normals(const oracle_scene *s, const Ray *ray, Counters *c) {
+    Its its;
+    c->closest++;
+    if (!scene_intersect(s, ray, &its, 0)) return v3(0, 0, 0);
+    return v3(fabsf(its.sh.n.x), fabsf(its.sh.n.y), fabsf(its.sh.n.z));
+}
+/* Warp::sampleUniformHemisphere (warp.cpp:25-42): rejection sampling in the
+ * cube, flipped into the hemisphere of the pole */
+static V3 uniform_hemisphere_rejection(Pcg *rng, V3 pole) {
+    V3 v;
+    do {
+        v.x = 1.f - 2.f * next1D(rng);
+        v.y = 1.f - 2.f * next1D(rng);
+        v.z = 1.f - 2.f * next1D(rng);
+    } while (vdot(v, v) > 1.f);
+    if (vdot(v, pole) < 0.f) v = vneg(v);
+    return vdivs(v, vnorm(v));
+}
+/* averagevisibility.cpp:16-27 */
+static V3 Li_av(const oracle_scene *s, Pcg *rng, const Ray *ray, Counters *c) {
+    Its its;
+    c->closest++;
+    if (!scene_intersect(s, ray, &its, 0)) return v3(1, 1, 1);
+    Ray r = ray_make(its.p, uniform_hemisphere_rejection(rng, its.sh.n), EPS, s->av_length);
+    c->shadow++;
+    return scene_occluded(s, &r) ? v3(0, 0, 0) : v3(1, 1, 1);
+}
+/* emission of the hit surface seen from ray.o (direct_*.cpp: EmitterQueryRecord(ray.o, its.p, n)) */
+static inline V3 hit_emission(const oracle_scene *s, const Its *its, V3 from) {
+    const Shape *sh = &s->shapes[its->shape];
+    if (sh->emitter < 0) return v3(0, 0, 0);
+    ERec r = erec_hit(from, its->p, its->sh.n);
+    return emitter_eval(&s->emitters[sh->emitter], &r);
+}
+/* direct.cpp:17-45 (DIRECT) and direct_ems.cpp:17-51 (DIRECT_EMS): every
+ * light, one shadow ray each.  `direct` passes an uninitialised sample to
+ * Emitter::sample (its scenes use point lights, which ignore it); here it is
+ * (0, 0) and no random number is drawn.  `direct` builds its BSDF record as
+ * (wi = light direction, wo = view direction), direct_ems the other way. */
+static V3 Li_direct_lights(const oracle_scene *s, Pcg *rng, const Ray *ray, Counters *c, int ems) {
+    Its its;
+    c->closest++;
+    if (!scene_intersect(s, ray, &its, 0)) return v3(0, 0, 0);
+    V3 color = v3(0, 0, 0);
+    if (ems) color = vadd(color, hit_emission(s, &its, ray->o));
+    const Bsdf *bsdf = &s->bsdfs[s->shapes[its.shape].bsdf];
+    for (uint32_t i = 0; i < s->nemitters; ++i) {
+        ERec er; memset(&er, 0, sizeof(er)); er.ref = its.p;
+        V2 zero = {0, 0};
+        V3 traced = emitter_sample(s, &s->emitters[i], &er, ems ? next2D(rng) : zero);
+        c->shadow++;
+        if (scene_occluded(s, &er.shadow)) continue;
+        V3 wi = to_local(&its.sh, er.wi), d = to_local(&its.sh, vneg(ray->d));
+        BRec br; memset(&br, 0, sizeof(br));
+        br.wi = ems ? d : wi; br.wo = ems ? wi : d; br.measure = M_SOLID_ANGLE; br.eta = 1.0f; br.uv = its.uv;
+        color = vadd(color, vmul(vmuls(bsdf_eval(bsdf, &br), wi.z), traced));
+    }
+    return color;
+}
+/* direct_mats.cpp:17-44 and direct_mis.cpp:17-85.  A BSDF sample of zero
+ * weight traces no ray (deviation D1: the reference traces along an
+ * unset bRec.wo and multiplies the result by zero). */
+static V3 Li_direct_mats_mis(const oracle_scene *s, Pcg *rng, const Ray *ray, Counters *c, int mis) {
+    Its its;
+    c->closest++;
+    if (!scene_intersect(s, ray, &its, 0)) return v3(0, 0, 0);
+    V3 color = hit_emission(s, &its, ray->o);
+    const Bsdf *bsdf = &s->bsdfs[s->shapes[its.shape].bsdf];
+    for (uint32_t i = 0; mis && i < s->nemitters; ++i) {
+        const Emitter *light = &s->emitters[i];
+        ERec er; memset(&er, 0, sizeof(er)); er.ref = its.p;
+        V3 traced = emitter_sample(s, light, &er, next2D(rng));
+        float pdf_em = emitter_pdf(s, light, &er);
+        c->shadow++;
+        if (scene_occluded(s, &er.shadow)) continue;
+        V3 wi = to_local(&its.sh, er.wi), d = to_local(&its.sh, vneg(ray->d));
+        BRec br; memset(&br, 0, sizeof(br));
+        br.wi = d; br.wo = wi; br.measure = M_SOLID_ANGLE; br.eta = 1.0f; br.uv = its.uv;
+        V3 f = bsdf_eval(bsdf, &br);
+        float pdf_mat = bsdf_pdf(bsdf, &br);
+        float w_em = pdf_mat + pdf_em > 0.f ? pdf_em / (pdf_mat + pdf_em) : pdf_em;
+        color = vadd(color, vmuls(vmul(vmuls(f, w_em), traced), wi.z));
+    }
+    BRec br; memset(&br, 0, sizeof(br));
+    br.wi = to_local(&its.sh, vneg(ray->d)); br.uv = its.uv;
+    V3 w = bsdf_sample(bsdf, &br, next2D(rng));
+    if (vzero(w)) return color;                                        /* D1 */
+    float pdf_mat = mis ? bsdf_pdf(bsdf, &br) : 0.0f;
+    Ray nr = ray_make(its.p, to_world(&its.sh, br.wo), EPS, F_INF);
+    Its ni;
+    c->closest++;
+    if (!scene_intersect(s, &nr, &ni, 0)) return color;
+    const Shape *nsh = &s->shapes[ni.shape];
+    if (nsh->emitter < 0) return color;
+    const Emitter *e = &s->emitters[nsh->emitter];
+    ERec er = erec_hit(its.p, ni.p, ni.sh.n);
+    V3 Le = emitter_eval(e, &er);
+    if (!mis) return vadd(color, vmul(w, Le));
+    float pdf_em = emitter_pdf(s, e, &er);
+    float w_mat = pdf_mat + pdf_em > 0.f ? pdf_mat / (pdf_mat + pdf_em) : 0.0f;
+    return vadd(color, vmul(vmuls(w, w_mat), Le));
+}
+
 static inline V3 Li(const oracle_scene *s, Pcg *rng, const Ray *ray, Counters *c) {
     switch (s->integrator) {
     case NORI_INTEGRATOR_PATH_MATS: return Li_mats(s, rng, ray, c);
     case NORI_INTEGRATOR_VOLUMETRIC: return Li_vol(s, rng, ray, c);
+    case NORI_INTEGRATOR_NORMALS: return Li_normals(s, ray, c);
+    case NORI_INTEGRATOR_AV: return Li_av(s, rng, ray, c);
+    case NORI_INTEGRATOR_DIRECT: return Li_direct_lights(s, rng, ray, c, 0);
+    case NORI_INTEGRATOR_DIRECT_EMS: return Li_direct_lights(s, rng, ray, c, 1);
+    case NORI_INTEGRATOR_DIRECT_MATS: return Li_direct_mats_mis(s, rng, ray, c, 0);
+    case NORI_INTEGRATOR_DIRECT_MIS: return Li_direct_mats_mis(s, rng, ray, c, 1);
     default: return Li_mis(s, rng, ray, c);
     }
 }
@@ -1222,14 +1399,99 @@ static inline V3 xform_vec(const float *m, V3 d) {
     return v3((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[4] * d.x + m[5] * d.y) + m[6] * d.z,
               (m[8] * d.x + m[9] * d.y) + m[10] * d.z);
 }
-/* perspective.cpp:90-112 */
-static Ray camera_ray(const oracle_scene *s, V2 ps) {
+/* Warp::squareToConcentricDisk (warp.cpp:143-162) and squareToUniformDisk
+ * (warp.cpp:53-58); cos/sin in single precision */
+static V2 sq_concentric_disk(V2 s) {
+    V2 o = {2.f * s.x - 1.f, 2.f * s.y - 1.f}, r0 = {0, 0};
+    if (o.x == 0.0f && o.y == 0.0f) return r0;
+    float theta, r;
+    if (fabsf(o.x) > fabsf(o.y)) { r = o.x; theta = F_PI * 0.25f * (o.y / o.x); }
+    else { r = o.y; theta = F_PI * 0.5f - F_PI * 0.25f * (o.x / o.y); }
+    V2 q = {r * cosf(theta), r * sinf(theta)};
+    return q;
+}
+static V2 sq_uniform_disk(V2 s) {
+    float angle = 2 * s.x * F_PI, size = sqrtf(s.y);
+    V2 q = {cosf(angle) * size, sinf(angle) * size};
+    return q;
+}
+/* Camera::sampleRay: PerspectiveCamera (perspective.cpp:90-112), ThinLensCamera
+ * (thinlens.cpp:120-147), AdvancedCamera (advancedCamera.cpp:85-157: barrel
+ * distortion by Newton iterations, uniform-disk lens, chromatic aberration
+ * shifting the focus point per colour channel).  *weight = the returned
+ * Color3f (1, or the unit vector of `channel` with chromatic aberration). */
+static Ray camera_sample(const oracle_scene *s, V2 ps, V2 ap, int channel, V3 *weight) {
     V3 nearP = xform_point(s->s2c, v3(ps.x * s->invW, ps.y * s->invH, 0.0f));
     V3 d = vnormalize(nearP);
+    *weight = v3(1, 1, 1);
+    float w = 0.0f;
+    int chroma = 0;
+    if (s->cam_type == NORI_CAMERA_ADVANCED) {
+        if (s->distortion[0] != 0.0f || s->distortion[1] != 0.0f) {
+            float k1 = s->distortion[0], k2 = s->distortion[1];
+            float qx = nearP.x / nearP.z, qy = nearP.y / nearP.z;
+            float y = sqrtf(qx * qx + qy * qy), r = y, r2, f, df;
+            int i = 0;
+            for (;;) {
+                r2 = r * r;
+                f = r * (1 + (k1 * r2) + k2 * (r2 * r2)) - y;
+                df = 1 + (3 * k1 * r2) + (5 * k2 * r2 * r2);
+                r = r - f / df;
+                if ((double)fabsf(f) < 1e-6 || i++ > 4) break;
+            }
+            float factor = r / y;
+            nearP.x *= factor; nearP.y *= factor;
+            d = vnormalize(nearP);
+        }
+        chroma = s->chromatic.x != 0.0f || s->chromatic.y != 0.0f || s->chromatic.z != 0.0f;
+        if (chroma) {
+            w = channel == 0 ? s->chromatic.x : (channel == 1 ? s->chromatic.y : s->chromatic.z);
+            *weight = v3(channel == 0, channel == 1, channel == 2);
+        }
+    }
     float invZ = 1.0f / d.z;
-    V3 o = xform_point(s->c2w, v3(0, 0, 0));
-    V3 dw = xform_vec(s->c2w, d);
+    V3 o, dw;
+    if (s->cam_type != NORI_CAMERA_PERSPECTIVE && (s->lens_radius > 0.0f || chroma)) {
+        V2 pl = s->cam_type == NORI_CAMERA_THINLENS ? sq_concentric_disk(ap) : sq_uniform_disk(ap);
+        pl.x *= s->lens_radius; pl.y *= s->lens_radius;
+        float ft = s->focal / d.z;
+        V3 pf = vmuls(d, ft);                                    /* Ray3f(0, d)(ft) */
+        if (s->cam_type == NORI_CAMERA_ADVANCED) {
+            float spx = ps.x - 0.5f * (float)s->W, spy = ps.y - 0.5f * (float)s->H;
+            float mx = (float)(s->W > s->H ? s->W : s->H);
+            spx /= mx; spy /= mx;
+            float sq = spx * spx + spy * spy;
+            float dx = (spx * sq) * w, dy = (spy * sq) * w;
+            pf = vadd(pf, v3(-dx, dy, 0.0f));
+        }
+        V3 lo = v3(pl.x, pl.y, 0.0f);
+        V3 nd = vnormalize(vsub(pf, lo));
+        o = xform_point(s->c2w, lo);
+        dw = xform_vec(s->c2w, nd);
+    } else {
+        o = xform_point(s->c2w, v3(0, 0, 0));
+        dw = xform_vec(s->c2w, d);
+    }
     return ray_make(o, dw, s->near_clip * invZ, s->far_clip * invZ);
+}
+static int has_chromatic(const oracle_scene *s) {
+    return s->cam_type == NORI_CAMERA_ADVANCED &&
+           (s->chromatic.x != 0.0f || s->chromatic.y != 0.0f || s->chromatic.z != 0.0f);
+}
+/* renderBlock's per-sample body (render.cpp:98-126) after the two 2D draws:
+ * one ray, or with chromatic aberration one ray per colour channel whose Li
+ * calls consume the sampler in turn; value = sum of weight * Li. */
+static V3 sample_value(const oracle_scene *s, Pcg *r, V2 ps, V2 ap, Counters *cnt) {
+    V3 wt;
+    if (!has_chromatic(s)) {
+        Ray ray = camera_sample(s, ps, ap, -1, &wt);
+        return vmul(wt, Li(s, r, &ray, cnt));
+    }
+    Ray rays[3]; V3 w[3];
+    for (int ch = 0; ch < 3; ++ch) rays[ch] = camera_sample(s, ps, ap, ch, &w[ch]);
+    V3 v[3];
+    for (int ch = 0; ch < 3; ++ch) v[ch] = vmul(w[ch], Li(s, r, &rays[ch], cnt));
+    return vadd(vadd(v[0], v[1]), v[2]);
 }
 
 /* ------------------------------------------------------------------ film */
@@ -1321,6 +1583,7 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
         const nori_shape_desc *sd = &d->shapes[i];
         Shape *sh = &s->shapes[i];
         sh->type = sd->type; sh->tri_offset = sd->tri_offset; sh->has_normals = sd->has_normals;
+        sh->has_uvs = sd->has_uvs;
         sh->center = v3(sd->center[0], sd->center[1], sd->center[2]); sh->radius = sd->radius;
         sh->bsdf = sd->bsdf; sh->emitter = sd->emitter;
         sh->prim_offset = off;
@@ -1361,7 +1624,16 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
     for (uint32_t i = 0; i < d->num_emitters; ++i) {
         if (d->emitters[i].type == NORI_EMITTER_ENVMAP) {
             if (env_build(&s->emitters[i], &d->emitters[i]) != NORI_OK) { oracle_scene_free(s); return NORI_ERR_INVALID; }
-        } else if (d->emitters[i].type != NORI_EMITTER_AREA) { oracle_scene_free(s); return NORI_ERR_UNSUPPORTED; }
+        } else if (d->emitters[i].type != NORI_EMITTER_AREA && d->emitters[i].type != NORI_EMITTER_POINT &&
+                   d->emitters[i].type != NORI_EMITTER_SPOT) { oracle_scene_free(s); return NORI_ERR_UNSUPPORTED; }
+        {
+            const nori_emitter_desc *ed = &d->emitters[i];
+            Emitter *e = &s->emitters[i];
+            e->pos = v3(ed->position[0], ed->position[1], ed->position[2]);
+            e->power = v3(ed->power[0], ed->power[1], ed->power[2]);
+            e->dir = v3(ed->direction[0], ed->direction[1], ed->direction[2]);
+            e->cos_fs = ed->cos_falloff_start; e->cos_tw = ed->cos_total_width;
+        }
         s->emitters[i].type = d->emitters[i].type;
         s->emitters[i].shape = d->emitters[i].shape;
         s->emitters[i].radiance = v3(d->emitters[i].radiance[0], d->emitters[i].radiance[1], d->emitters[i].radiance[2]);
@@ -1382,6 +1654,10 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
     s->filter[NORI_FILTER_RESOLUTION] = 0.0f;
     s->lookup_factor = NORI_FILTER_RESOLUTION / s->filter_radius;
     s->integrator = d->integrator;
+    s->av_length = d->av_length;
+    s->cam_type = c->camera_type; s->lens_radius = c->lens_radius; s->focal = c->focal_distance;
+    s->distortion[0] = c->distortion[0]; s->distortion[1] = c->distortion[1];
+    s->chromatic = v3(c->chromatic[0], c->chromatic[1], c->chromatic[2]);
     s->has_medium = d->medium.present;
     if (s->has_medium) {
         const nori_medium_desc *m = &d->medium;
@@ -1393,7 +1669,9 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
     } else if (s->integrator == NORI_INTEGRATOR_VOLUMETRIC) {
         oracle_scene_free(s); return NORI_ERR_INVALID;
     }
-    if (s->nemitters == 0) { oracle_scene_free(s); return NORI_ERR_INVALID; }
+    if (s->nemitters == 0 && s->integrator != NORI_INTEGRATOR_NORMALS && s->integrator != NORI_INTEGRATOR_AV) {
+        oracle_scene_free(s); return NORI_ERR_INVALID;
+    }
     if (bvh_build(s) != 0) { oracle_scene_free(s); return NORI_ERR_OOM; }
     *out = s;
     return NORI_OK;
@@ -1471,9 +1749,8 @@ static void render_block(RenderJob *j, uint32_t bid, Block *blk, Counters *cnt, 
             }
             V2 jit = next2D(r);
             V2 ps = {(float)(x + blk->ox) + jit.x, (float)(y + blk->oy) + jit.y};
-            (void)next2D(r);                                    /* apertureSample, render.cpp:99 */
-            Ray ray = camera_ray(s, ps);
-            V3 val = Li(s, r, &ray, cnt);                        /* camera weight 1 */
+            V2 ap = next2D(r);                                   /* apertureSample, render.cpp:99 */
+            V3 val = sample_value(s, r, ps, ap, cnt);
             if (!block_put(s, blk, ps, val)) (*inval)++;
         }
 }
@@ -1622,9 +1899,8 @@ int oracle_wave_samples(const oracle_scene *s, uint64_t seed, const uint64_t *id
         Pcg r; wave_seed(&r, seed, ids[i]);
         V2 jit = next2D(&r);
         V2 ps = {(float)x + jit.x, (float)y + jit.y};
-        (void)next2D(&r);
-        Ray ray = camera_ray(s, ps);
-        V3 L = Li(s, &r, &ray, &cnt);
+        V2 ap = next2D(&r);
+        V3 L = sample_value(s, &r, ps, ap, &cnt);
         float *o = out + 5 * (size_t)i;
         o[0] = ps.x; o[1] = ps.y; o[2] = L.x; o[3] = L.y; o[4] = L.z;
     }
@@ -1650,9 +1926,8 @@ int oracle_scene_ttest(const oracle_scene *s, uint32_t n, double *mean, double *
     for (uint32_t k = 0; k < n; ++k) {
         V2 a = next2D(&r);
         V2 ps = {a.x * (float)s->W, a.y * (float)s->H};
-        (void)next2D(&r);
-        Ray ray = camera_ray(s, ps);
-        V3 val = Li(s, &r, &ray, &cnt);
+        V2 ap = next2D(&r);
+        V3 val = sample_value(s, &r, ps, ap, &cnt);
         double res = (double)lum(val);
         double delta = res - m;
         m += delta / (double)(k + 1);

@@ -122,3 +122,28 @@ def envmap_scene(outdir, width=128, height=128, spp=16, integrator="path_mis", r
     with open(xml, "w") as f:
         f.write(src)
     return xml
+
+
+def cbox_variant(outdir, name, integrator="path_mis", camera_type="perspective", camera_props="",
+                 integrator_props="", extra="", width=0, height=0):
+    """scenes/pa4/cbox/cbox_path_mis.xml with another integrator and camera
+    plugin (thinlens.cpp / advancedCamera.cpp properties in `camera_props`,
+    e.g. lensRadius / focalDist / distortion / chromaticAberation) and extra
+    scene children (free-standing point/spot emitters)."""
+    import re
+
+    os.makedirs(outdir, exist_ok=True)
+    src = open(os.path.join(CBOX, "cbox_path_mis.xml")).read()
+    src = src.replace('value="meshes/', f'value="{os.path.join(CBOX, "meshes")}/')
+    src = src.replace('<integrator type="path_mis"/>',
+                      f'<integrator type="{integrator}">{integrator_props}</integrator>')
+    src = src.replace('<camera type="perspective">', f'<camera type="{camera_type}">{camera_props}')
+    if width:
+        src = re.sub(r'<integer name="width" value="\d+"/>', f'<integer name="width" value="{width}"/>', src)
+    if height:
+        src = re.sub(r'<integer name="height" value="\d+"/>', f'<integer name="height" value="{height}"/>', src)
+    src = src.replace("</scene>", extra + "\n</scene>")
+    xml = os.path.join(outdir, f"{name}.xml")
+    with open(xml, "w") as f:
+        f.write(src)
+    return xml

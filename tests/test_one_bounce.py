@@ -1,0 +1,152 @@
+"""Oracle pinning for the widened plugins: the one-bounce
+integrators (normals, av, direct, direct_ems, direct_mats, direct_mis), point and
+spot lights, the checkerboard albedo texture and the thinlens / advancedCamera
+ray generators.  No GPU needed.
+
+Fixtures (all from the reference's own scene tree, copied as data):
+* Student-t tests scenes/pa1/test-av.xml and scenes/pa1/test-direct.xml
+  (ttest.cpp:147-194; references 0.894/0.707/0.707/1 and 1/0.06317/0/1.06317).
+* golden renders of the course solution: scenes/pa1/ref/sphere-{analytic,mesh,
+  texture}.exr, scenes/pa3/sphere/ref/*.exr, scenes/pa3/odyssey/ref/*.exr,
+  scenes/pa3/veach_mi/ref/veach_mis_128spp.exr.  Compared in expectation: the
+  oracle at a few spp against the golden at its own spp, by channel means and
+  16x16-block relMSE.  Measured (block stream, 8 threads): channel means within
+  0.1 % (veach 0.7 % at 8 spp: the small bright spheres), block relMSE <= 8e-4.
+* thinlens / advancedCamera have no golden render in the reference tree:
+  they are pinned by their degenerate cases (lensRadius 0, no distortion, no
+  chromatic aberration == perspective, bit for bit) and, on the GPU side, by
+  parity with this oracle (tests/test_gpu_one_bounce.py) -- parity unpinned
+  beyond that.
+"""
+import numpy as np
+import pytest
+
+import nori_amd
+import pyoracle
+import synth
+from conftest import scene_path
+from nori_test_util import load_test_scenes, parse_test_xml, students_t_test
+
+
+@pytest.mark.parametrize("xml", ["test-av.xml", "test-direct.xml"])
+def test_pa1_ttests(built, tmp_path, xml):
+    path = scene_path("pa1", xml)
+    meta = parse_test_xml(path)
+    scenes = load_test_scenes(path, tmp_path)
+    refs = meta["references"]
+    assert len(refs) == len(scenes)
+    fails = []
+    for (scene, integ), ref in zip(scenes, refs):
+        mean, var = pyoracle.OracleScene(scene).ttest(meta["sampleCount"])
+        ok, p = students_t_test(mean, var, ref, meta["sampleCount"], meta["significanceLevel"], len(refs))
+        if not ok:
+            fails.append((integ, ref, mean, p))
+    assert not fails, fails
+
+
+def _blocks(a, k):
+    h, w = a.shape[0] // k * k, a.shape[1] // k * k
+    return a[:h, :w].reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+
+
+# (scene, golden, oracle spp, channel-mean rel tol, 16x16-block relMSE tol)
+GOLDEN_CASES = [
+    ("pa1/sphere-analytic.xml", "pa1/ref/sphere-analytic.exr", 4, 2e-3, 1e-4),
+    ("pa1/sphere-mesh.xml", "pa1/ref/sphere-mesh.exr", 4, 2e-3, 1e-4),
+    ("pa1/sphere-texture.xml", "pa1/ref/sphere-texture.exr", 4, 2e-3, 1e-4),
+    ("pa3/sphere/point_ems.xml", "pa3/sphere/ref/point_ems.exr", 4, 2e-3, 1e-5),
+    ("pa3/sphere/sphere_ems.xml", "pa3/sphere/ref/sphere_ems.exr", 16, 5e-3, 2e-3),
+    ("pa3/sphere/sphere_mats.xml", "pa3/sphere/ref/sphere_mats.exr", 16, 5e-3, 4e-3),
+    ("pa3/sphere/sphere_mesh_ems.xml", "pa3/sphere/ref/sphere_mesh_ems.exr", 16, 5e-3, 2e-3),
+    ("pa3/odyssey/odyssey_ems.xml", "pa3/odyssey/ref/odyssey_ems_64spp.exr", 16, 5e-3, 2e-3),
+    ("pa3/odyssey/odyssey_mats.xml", "pa3/odyssey/ref/odyssey_mats_64spp.exr", 16, 5e-3, 2e-3),
+    ("pa3/odyssey/odyssey_mis.xml", "pa3/odyssey/ref/odyssey_mis_32spp.exr", 16, 5e-3, 2e-3),
+    ("pa3/veach_mi/veach_mis.xml", "pa3/veach_mi/ref/veach_mis_128spp.exr", 8, 2e-2, 2e-3),
+]
+
+
+@pytest.mark.parametrize("xml,golden,spp,mean_tol,block_tol", GOLDEN_CASES, ids=[c[0] for c in GOLDEN_CASES])
+def test_oracle_matches_reference_golden(built, xml, golden, spp, mean_tol, block_tol):
+    s = nori_amd.load_scene(scene_path(xml), 0, 0, spp)
+    img = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="block", threads=8))
+    ref = nori_amd.read_exr(scene_path(golden))
+    assert img.shape == ref.shape
+    m, mr = img.mean(axis=(0, 1)), ref.mean(axis=(0, 1))
+    rel = np.abs(m - mr) / np.maximum(mr, 1e-3)
+    bi, br = _blocks(img, 16), _blocks(ref, 16)
+    rb = float(np.mean((bi - br) ** 2 / (br ** 2 + 1e-2)))
+    print(f"{xml}: means {m} golden {mr}, 16x16-block relMSE {rb:.2e}")
+    assert np.all(rel < mean_tol), (m, mr)
+    assert rb < block_tol
+
+
+def test_loader_checkerboard_and_lights(built):
+    s = nori_amd.load_scene(scene_path("pa1", "sphere-texture.xml"))
+    b = s.bsdfs()[0]
+    assert b.albedo_texture == nori_amd._abi.TEXTURE_CHECKERBOARD
+    assert list(b.albedo) == pytest.approx([0.8] * 3) and list(b.tex_value2) == pytest.approx([0.2] * 3)
+    assert list(b.tex_scale) == pytest.approx([0.1, 0.2]) and list(b.tex_delta) == [0.0, 0.0]
+    e = s.emitters()[0]
+    assert e.type == nori_amd._abi.EMITTER_POINT and e.shape == -1
+    assert list(e.position) == [3.0, 7.0, 10.0] and list(e.power) == [2000.0] * 3
+    ss = nori_amd.load_scene(scene_path("project", "spotlight", "sphere-texture.xml"))
+    sp = ss.emitters()[0]  # a view into ss's memory: ss must stay alive
+    assert sp.type == nori_amd._abi.EMITTER_SPOT
+    assert list(sp.direction) == [0.0, 0.0, -1.0]
+    assert sp.cos_falloff_start == 1.0
+    assert sp.cos_total_width == pytest.approx(np.cos(np.radians(20.0)), rel=1e-6)
+
+
+def test_loader_cameras(built, tmp_path):
+    xml = synth.cbox_variant(str(tmp_path), "adv", camera_type="advancedCamera",
+                             camera_props='<float name="lensRadius" value="0.05"/><float name="focalDist" value="4.5"/>'
+                                          '<vector name="distortion" value="0.3, 0.1"/>'
+                                          '<vector name="chromaticAberation" value="4, 2, 3.3"/>',
+                             integrator="direct_mis", width=64, height=48)
+    sa = nori_amd.load_scene(xml)
+    c = sa.desc.camera
+    assert c.camera_type == nori_amd._abi.CAMERA_ADVANCED
+    assert c.lens_radius == pytest.approx(0.05) and c.focal_distance == pytest.approx(4.5)
+    assert list(c.distortion) == pytest.approx([0.3, 0.1]) and list(c.chromatic) == pytest.approx([4, 2, 3.3])
+    xml = synth.cbox_variant(str(tmp_path), "thin", camera_type="thinlens", width=64, height=48)
+    st = nori_amd.load_scene(xml)
+    c = st.desc.camera
+    assert c.camera_type == nori_amd._abi.CAMERA_THINLENS
+    assert c.lens_radius == 0.0 and c.focal_distance == 1.0  # thinlens.cpp:51-52 defaults
+
+
+@pytest.mark.parametrize("camera", ["thinlens", "advancedCamera"])
+def test_degenerate_cameras_equal_perspective(built, tmp_path, camera):
+    """lensRadius 0 and no distortion / aberration: the same rays as
+    PerspectiveCamera, so the oracle film is bit-identical."""
+    base = nori_amd.load_scene(synth.cbox_variant(str(tmp_path), "p", width=40, height=32), 0, 0, 2)
+    alt = nori_amd.load_scene(synth.cbox_variant(str(tmp_path), "c", camera_type=camera, width=40, height=32), 0, 0, 2)
+    a = pyoracle.OracleScene(base).render(rng="wave")
+    b = pyoracle.OracleScene(alt).render(rng="wave")
+    assert np.array_equal(a, b)
+
+
+def test_thinlens_defocus_keeps_the_mean(built, tmp_path):
+    """A lens blurs the image but (the scene being lit uniformly enough over the
+    aperture) keeps its mean: a statistical check of the lens sampling."""
+    sharp = nori_amd.load_scene(synth.cbox_variant(str(tmp_path), "p", width=48, height=48), 0, 0, 32)
+    blur = nori_amd.load_scene(synth.cbox_variant(
+        str(tmp_path), "t", camera_type="thinlens", width=48, height=48,
+        camera_props='<float name="lensRadius" value="0.1"/><float name="focalDist" value="2.0"/>'), 0, 0, 32)
+    a = nori_amd.develop(sharp, pyoracle.OracleScene(sharp).render(rng="wave"))
+    b = nori_amd.develop(blur, pyoracle.OracleScene(blur).render(rng="wave"))
+    assert not np.allclose(a, b)
+    assert np.allclose(a.mean(axis=(0, 1)), b.mean(axis=(0, 1)), rtol=0.06)
+    # defocus removes high-frequency detail: smaller mean gradient
+    ga = np.abs(np.diff(a, axis=1)).mean()
+    gb = np.abs(np.diff(b, axis=1)).mean()
+    assert gb < ga
+
+
+def test_av_and_normals_need_no_emitter(built, tmp_path):
+    xml = synth.cbox_variant(str(tmp_path), "av", integrator="av", integrator_props='<float name="length" value="0.5"/>',
+                             width=32, height=32)
+    s = nori_amd.load_scene(xml, 0, 0, 4)
+    assert s.integrator == "av" and s.desc.av_length == pytest.approx(0.5)
+    img = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
+    assert np.isfinite(img).all() and 0.0 < img.mean() <= 1.0
