@@ -59,6 +59,14 @@ hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &
                          hipStream_t st);
 // One-bounce integrators (normals, av, direct, direct_ems/mats/mis): one thread
 // per work id of wd (pass-major, pixels in wd.pixels order) writes its record.
+// Persistent BVH traversal (k_trace_pt): `blocks` resident work-groups pull
+// queue segments through ctr[0..1] (zero before the first launch; each launch
+// leaves them zero).  Stacks 8, 16, 32 only (BVH scenes).
+hipError_t launch_extend_pt(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
+                            uint32_t *ctr, uint32_t blocks, hipStream_t st);
+hipError_t launch_shadow_pt(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
+                            int stack, uint32_t *ctr, uint32_t blocks, hipStream_t st);
+int pt_blocks_per_cu(int stack, bool any);
 hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack, hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);

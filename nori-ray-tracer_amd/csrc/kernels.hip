@@ -461,6 +461,253 @@ ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *sh
     }
 }
 
+// ------------------------------------------------------------------ persistent traversal
+// BVH scenes: incoherent rays make a one-ray-per-thread wave run as long as
+// its longest ray (measured on C3: ~13 node/leaf rounds per wave for ~5 per
+// ray).  The persistent kernels below keep a fixed set of waves resident:
+//  * dynamic fetch -- a wave owns one queue segment at a time (claimed with
+//    one atomic per segment) and hands its next entries to idle lanes
+//    whenever at least kRefill lanes are idle, so lanes do not idle until the
+//    wave's longest ray ends (Aila & Laine 2009, "persistent while-while");
+//  * while-while with postponed leaves -- the node loop runs until every
+//    busy lane holds a leaf, then the leaf loop intersects them together, so
+//    node and leaf code do not alternate inside a diverged wave.
+// The candidate primitives of a ray are those of traverse() (same box test,
+// same key culling against the current closest t), so t and the hit are the
+// same; only the order among equal-t primitives may differ.
+// ctr[0]: next segment, ctr[1]: retired waves; the last wave to retire
+// resets both, so the next launch starts from zero without a memset.
+#ifndef NORI_PT_REFILL
+#define NORI_PT_REFILL 16
+#endif
+constexpr int kRefill = NORI_PT_REFILL;
+#ifndef NORI_PT_SPEC  // 1: postpone leaves until every busy lane holds one; 0: intersect as soon as one does
+#define NORI_PT_SPEC 1
+#endif
+#ifdef NORI_PT_WAVES
+#define NORI_TRACE_ATTR_PT __attribute__((amdgpu_waves_per_eu(NORI_PT_WAVES)))
+#else
+#define NORI_TRACE_ATTR_PT
+#endif
+
+template <bool ANY>
+struct PtJob {
+    const float4 *ray_o, *ray_d;
+    float4 *hit;            // closest hit (extension rays)
+    const float4 *payload;  // shadow rays: contribution, work id in w
+    float4 *rec;            // shadow rays: sample records
+};
+
+template <int STACK, bool ANY>
+__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(DevScene S, PtJob<ANY> J,
+                                                                             const uint32_t *cnt, uint32_t G,
+                                                                             uint32_t *ctr) {
+    __shared__ uint32_t stk_lds[stack_words(STACK) * kTraceBlock];
+    uint32_t *stk = stk_lds + threadIdx.x;
+    constexpr int L = stack_lds_entries(STACK);
+    uint32_t spill[kTraceSpill];
+    float spillk[kTraceSpill];
+    const uint32_t lane = lane_id();
+    // wave-uniform work cursor: current segment, its count, next entry
+    uint32_t seg = 0, seg_n = 0, seg_pos = 0;
+    bool have_seg = false;  // becomes false for good once the segments run out
+    bool more = true;
+    // lane state
+    bool active = false, has_ref = false, has_leaf = false, found = false;
+    uint32_t q = 0, ref = 0, leaf = 0, pb = 0xFFFFFFFFu;
+    int sp = 0;
+    TRay r;
+    r.o = r.d = r.rcp = V3{0, 0, 0};
+    r.mint = r.maxt = 0.0f;
+    float tb = INF_F, ub = 0.0f, vb = 0.0f;
+    auto push = [&](uint32_t v, float k) {
+        if (sp < L) {
+            stk[sp * kTraceBlock] = v;
+            stk[(L + sp) * kTraceBlock] = __float_as_uint(k);
+        } else {
+            spill[sp - L] = v;
+            spillk[sp - L] = k;
+        }
+        ++sp;
+    };
+    // next stack entry whose box starts within the current closest hit
+    auto pop = [&]() -> bool {
+        while (sp > 0) {
+            --sp;
+            const uint32_t v = sp < L ? stk[sp * kTraceBlock] : spill[sp - L];
+            const float key = sp < L ? __uint_as_float(stk[(L + sp) * kTraceBlock]) : spillk[sp - L];
+            if (!(key > r.maxt)) {
+                ref = v;
+                return true;
+            }
+        }
+        return false;
+    };
+    for (;;) {
+        // ---- refill idle lanes from the wave's segment(s)
+        uint64_t idle = __ballot(!active);
+        if (more && (uint32_t)__popcll(idle) >= (uint32_t)kRefill) {
+            uint32_t need = (uint32_t)__popcll(idle), given = 0;
+            const uint32_t my = rank_in(idle);
+            while (need > 0) {
+                if (!have_seg || seg_pos >= seg_n) {
+                    uint32_t s = 0;
+                    if (lane == 0) s = atomicAdd(&ctr[0], 1u);
+                    s = __builtin_amdgcn_readfirstlane(s);
+                    if (s >= G) {
+                        more = false;
+                        break;
+                    }
+                    seg = s;
+                    seg_n = cnt[s];
+                    seg_pos = 0;
+                    have_seg = true;
+                    continue;
+                }
+                const uint32_t take = min(need, seg_n - seg_pos);
+                if (!active && my >= given && my < given + take) {
+                    q = seg * kSeg + seg_pos + (my - given);
+                    const float4 a = J.ray_o[q], b = J.ray_d[q];
+                    r.o = ld3(a);
+                    r.d = ld3(b);
+                    r.mint = a.w;
+                    r.maxt = b.w;
+                    if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
+                    r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+                    tb = INF_F;
+                    pb = 0xFFFFFFFFu;
+                    ub = vb = 0.0f;
+                    found = false;
+                    sp = 0;
+                    ref = 0;
+                    has_ref = !(r.maxt < r.mint);
+                    has_leaf = false;
+                    active = true;
+                }
+                given += take;
+                need -= take;
+                seg_pos += take;
+            }
+        }
+        if (!__any(active)) {
+            if (!more) break;
+            continue;
+        }
+        // ---- node loop: descend until every busy lane holds a leaf
+        for (;;) {
+            if (active && has_ref && (ref & 0x80000000u) && !has_leaf) {
+                leaf = ref;
+                has_leaf = true;
+                has_ref = pop();
+            }
+            const bool in_node = active && has_ref && !(ref & 0x80000000u);
+            if (!__any(in_node)) break;
+            if (NORI_PT_SPEC ? __all(!active || has_leaf || !has_ref) : __any(active && has_leaf)) break;
+            if (in_node) {
+                const float4 *nd = S.nodes + 8 * (size_t)ref;
+                const float4 mnx = gld(nd), mny = gld(nd + 1), mnz = gld(nd + 2), mxx = gld(nd + 3),
+                             mxy = gld(nd + 4), mxz = gld(nd + 5), rf = gld(nd + 6);
+                float k0, k1, k2, k3;
+                const bool h0 = box_test(make_float4(mnx.x, mny.x, mnz.x, 0), make_float4(mxx.x, mxy.x, mxz.x, 0), r, k0);
+                const bool h1 = box_test(make_float4(mnx.y, mny.y, mnz.y, 0), make_float4(mxx.y, mxy.y, mxz.y, 0), r, k1);
+                const bool h2 = box_test(make_float4(mnx.z, mny.z, mnz.z, 0), make_float4(mxx.z, mxy.z, mxz.z, 0), r, k2);
+                const bool h3 = box_test(make_float4(mnx.w, mny.w, mnz.w, 0), make_float4(mxx.w, mxy.w, mxz.w, 0), r, k3);
+                k0 = h0 ? k0 : INF_F;
+                k1 = h1 ? k1 : INF_F;
+                k2 = h2 ? k2 : INF_F;
+                k3 = h3 ? k3 : INF_F;
+                const int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+                if (nh > 0) {
+                    uint32_t c0 = __float_as_uint(rf.x), c1 = __float_as_uint(rf.y), c2 = __float_as_uint(rf.z),
+                             c3 = __float_as_uint(rf.w);
+                    bool m0 = !h0, m1 = !h1, m2 = !h2, m3 = !h3;
+                    auto cs = [](float &ka, uint32_t &ca, bool &ma, float &kb, uint32_t &cb, bool &mb) {
+                        const bool sw = ma > mb || (ma == mb && kb < ka);
+                        const float tk = ka;
+                        const uint32_t tc = ca;
+                        const bool tm = ma;
+                        ka = sw ? kb : ka;
+                        kb = sw ? tk : kb;
+                        ca = sw ? cb : ca;
+                        cb = sw ? tc : cb;
+                        ma = sw ? mb : ma;
+                        mb = sw ? tm : mb;
+                    };
+                    cs(k0, c0, m0, k1, c1, m1);
+                    cs(k2, c2, m2, k3, c3, m3);
+                    cs(k0, c0, m0, k2, c2, m2);
+                    cs(k1, c1, m1, k3, c3, m3);
+                    cs(k1, c1, m1, k2, c2, m2);
+                    if (nh > 3) push(c3, k3);
+                    if (nh > 2) push(c2, k2);
+                    if (nh > 1) push(c1, k1);
+                    ref = c0;
+                } else {
+                    has_ref = pop();
+                }
+            }
+        }
+        // ---- leaf loop: intersect the postponed leaves (and leaves reached next)
+        for (;;) {
+            const bool lf = active && has_leaf;
+            if (!__any(lf)) break;
+            if (lf) {
+                const uint32_t start = leaf & 0x1FFFFFFu, end = start + ((leaf >> 25) & 63u) + 1u;
+                for (uint32_t i = start; i < end; ++i) {
+                    const float4 *p = S.prims + 3 * (size_t)i;
+                    const float4 p0 = gld(p), p1 = gld(p + 1);
+                    float t = 0, u = 0, v = 0;
+                    bool h;
+                    if (__float_as_uint(p1.w) == 0u) {
+                        const float4 p2 = gld(p + 2);
+                        h = tri_hit(p0, p1, p2, r, t, u, v);
+                    } else {
+                        h = sphere_hit(p0, p1, r, t);
+                        u = v = 0.0f;
+                    }
+                    if (h) {
+                        found = true;
+                        if (ANY) break;
+                        r.maxt = tb = t;
+                        ub = u;
+                        vb = v;
+                        pb = __float_as_uint(p0.w);
+                    }
+                }
+                has_leaf = false;
+                if (ANY && found) has_ref = false;
+                if (has_ref && (ref & 0x80000000u)) {
+                    leaf = ref;
+                    has_leaf = true;
+                    has_ref = pop();
+                }
+            }
+        }
+        // ---- retire finished rays
+        if (active && !has_ref && !has_leaf) {
+            if (ANY) {
+                if (!found) {
+                    const float4 c = J.payload[q];
+                    const uint32_t w = __float_as_uint(c.w);
+                    const float4 Lr = J.rec[w];
+                    J.rec[w] = make_float4(Lr.x + c.x, Lr.y + c.y, Lr.z + c.z, Lr.w);
+                }
+            } else {
+                J.hit[q] = make_float4(tb, __uint_as_float(pb), ub, vb);
+            }
+            active = false;
+        }
+    }
+    // the last wave of the launch to retire resets the work counters
+    if (lane == 0) {
+        const uint32_t waves = gridDim.x * (kTraceBlock / 64);
+        if (atomicAdd(&ctr[1], 1u) == waves - 1) {
+            atomicExch(&ctr[0], 0u);
+            atomicExch(&ctr[1], 0u);
+        }
+    }
+}
+
 #ifdef NORI_TRACE_WAVES
 #define NORI_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(NORI_TRACE_WAVES)))
 #else
@@ -1909,6 +2156,44 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     }
     return hipGetLastError();
+}
+
+template <bool ANY>
+static hipError_t pt_dispatch(const DevScene &S, const PtJob<ANY> &J, const uint32_t *cnt, uint32_t G, int stack,
+                              uint32_t *ctr, uint32_t blocks, hipStream_t st) {
+    const dim3 g(blocks), b(kTraceBlock);
+    switch (stack) {
+    case 8: hipLaunchKernelGGL((k_trace_pt<8, ANY>), g, b, 0, st, S, J, cnt, G, ctr); break;
+    case 16: hipLaunchKernelGGL((k_trace_pt<16, ANY>), g, b, 0, st, S, J, cnt, G, ctr); break;
+    case 32: hipLaunchKernelGGL((k_trace_pt<32, ANY>), g, b, 0, st, S, J, cnt, G, ctr); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_extend_pt(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
+                            uint32_t *ctr, uint32_t blocks, hipStream_t st) {
+    PtJob<false> J{q.ray_o, q.ray_d, q.hit, nullptr, nullptr};
+    return pt_dispatch<false>(S, J, cnt, G, stack, ctr, blocks, st);
+}
+hipError_t launch_shadow_pt(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
+                            int stack, uint32_t *ctr, uint32_t blocks, hipStream_t st) {
+    PtJob<true> J{sq.ray_o, sq.ray_d, nullptr, sq.payload, rec};
+    return pt_dispatch<true>(S, J, shcnt, G, stack, ctr, blocks, st);
+}
+// Resident work-groups per CU of the persistent traversal kernel.
+int pt_blocks_per_cu(int stack, bool any) {
+    int n = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (stack) {
+    case 8: e = any ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<8, true>, kTraceBlock, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<8, false>, kTraceBlock, 0); break;
+    case 16: e = any ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<16, true>, kTraceBlock, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<16, false>, kTraceBlock, 0); break;
+    case 32: e = any ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<32, true>, kTraceBlock, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<32, false>, kTraceBlock, 0); break;
+    default: break;
+    }
+    return e == hipSuccess ? n : 0;
 }
 
 hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st) {

@@ -199,6 +199,8 @@ struct nori_gpu_ctx {
     std::atomic<float> progress{1.0f};
     // render state
     DevBuf q[2][6], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
+    DevBuf ptctr;                    // persistent traversal work counters, 4 per part
+    uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
     uint32_t *pinned_dev = nullptr;  // device view of `pinned`
@@ -642,6 +644,28 @@ bool overlap_splat() {
     const char *e = std::getenv("NORI_SPLAT_OVERLAP");
     return !(e && e[0] == '0');
 }
+// NORI_PT=1: persistent traversal of the BVH scenes (k_trace_pt) with a grid
+// of the device's resident work-groups times NORI_PT_OCC (default 1).  Off by
+// default: interleaved A/B on MI355X (C3 height field, table scene) measured
+// -13..+3 % on C3 and -10..+7 % on the table against the one-ray-per-thread
+// launches, i.e. no reliable gain.
+void setup_persistent(nori_gpu_ctx &c) {
+    c.pt_grid[0] = c.pt_grid[1] = 0;
+    const char *e = std::getenv("NORI_PT");
+    if (c.stack == 0 || !(e && e[0] == '1')) return;
+    if (c.stack != 8 && c.stack != 16 && c.stack != 32) return;
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
+    const char *o = std::getenv("NORI_PT_OCC");
+    double occ = o ? std::atof(o) : 1.0;
+    if (!(occ > 0.0 && occ <= 1.0)) occ = 1.0;
+    for (int k = 0; k < 2; ++k) {
+        const int per_cu = pt_blocks_per_cu(c.stack, k == 1);
+        c.pt_grid[k] = (uint32_t)std::max(1.0, occ * per_cu * cus);
+    }
+    c.ptctr.ensure(4 * 4 * kMaxParts);
+    HIP_TRY(hipMemset(c.ptctr.p, 0, 4 * 4 * kMaxParts));
+}
 
 // normals / av / direct*: no path pool -- per chunk of passes, k_direct runs
 // every sample start to end and writes its record, then k_splat filters them.
@@ -906,9 +930,17 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                     HIP_TRY(hipEventRecord(c.fork, c.stream));
                     for (uint32_t k = 1; k < parts; ++k) HIP_TRY(hipStreamWaitEvent(c.parts[k], c.fork, 0));
                 }
+                uint32_t *ctr = c.pt_grid[0] ? c.ptctr.as<uint32_t>() + 4 * h : nullptr;
                 if (!fused)
-                    timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st); });
-                timed_on(st, 1, [&] { return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st); });
+                    timed_on(st, 0, [&] {
+                        return ctr ? launch_extend_pt(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, ctr, c.pt_grid[0], st)
+                                   : launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st);
+                    });
+                timed_on(st, 1, [&] {
+                    return ctr ? launch_shadow_pt(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, ctr + 2,
+                                                  c.pt_grid[1], st)
+                               : launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st);
+                });
             }
             ++iters;
             // an event every `every` iterations (each record adds a gap
@@ -1117,6 +1149,7 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         upload_scene(*c, *d);
+        setup_persistent(*c);
         *out = c.release();
         return NORI_OK;
     });
