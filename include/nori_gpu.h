@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define NORI_GPU_ABI_VERSION 2
+#define NORI_GPU_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define NORI_OK               0
@@ -208,6 +208,16 @@ int nori_filter_table(const nori_scene_desc *scene, float table[NORI_FILTER_RESO
 int nori_film_develop(const nori_scene_desc *scene, const float *rgbw, float *rgb);
 /* Write an RGB float image as an uncompressed scanline OpenEXR file. */
 int nori_write_exr(const char *path, const float *rgb, int width, int height);
+/* Bitmap::saveToLDR (bitmap.cpp:109-139): sRGB transfer curve, x255 + 0.5,
+ * clamp to [0, 255], 8-bit RGB PNG (zlib deflate, filter type 0). */
+int nori_write_png(const char *path, const float *rgb, int width, int height);
+/* Variance of each pixel's mean radiance from the statistics of
+ * render_desc.variance_out (H x W x 8): out (H x W x 3) =
+ * (sum L^2 - (sum L)^2 / n) / (n (n - 1)) per channel, in double precision;
+ * 0 where n < 2.  The reference's own estimator (render.cpp:235-247,
+ * 263-276: the spread of the running mean over the passes) does not estimate
+ * the pixel variance; this one does (deviation D5). */
+int nori_film_variance(const nori_scene_desc *scene, const float *stats, float *out);
 /* Read the R, G, B planes of a scanline OpenEXR file (NONE/ZIPS/ZIP, HALF or
  * FLOAT) <- Bitmap::Bitmap (bitmap.cpp:23-80).  Call with rgb = NULL to get
  * the size, then with a buffer of 3*width*height floats (row-major). */
@@ -240,6 +250,12 @@ typedef struct nori_gpu_render_desc {
     int32_t output_on_device;     /* rgbw_out is a device pointer on ctx device */
     uint32_t path_pool;           /* paths in flight (0 = default)              */
     int32_t timing;               /* nonzero: HIP events around every launch    */
+    /* Optional per-pixel sample statistics, H x W x 8 floats ADDED into
+     * (host or device memory like rgbw_out): sum of L (r, g, b), sum of L^2
+     * (r, g, b), valid sample count, 0 -- of every valid sample in the pixel
+     * it was taken in (unfiltered).  nori_film_variance turns them into the
+     * variance of the pixel mean.  NULL: not collected. */
+    float *variance_out;
 } nori_gpu_render_desc;
 
 typedef struct nori_gpu_stats {

@@ -142,6 +142,7 @@ struct WorkDesc {
     uint32_t *done_flag;     // host-mapped: set when the last segment exhausts its stream
     uint32_t rot;            // stream rotation (stream_rotation)
     uint32_t b0;             // global id of the launch's segment 0 (pool halves on two streams)
+    float *var;              // per-pixel sample statistics W x H x 8 (sum L, sum L^2, n) or null
 };
 // Round j hands segment b the chunk (b + j*rot) mod G of that round.  Path
 // lengths vary strongly across the image, so every segment's stream must

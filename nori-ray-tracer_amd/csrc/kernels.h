@@ -36,6 +36,7 @@ struct SplatDesc {
     uint32_t passes_per_wg;   // passes folded by one work-group
     const int4 *blocks;       // (ox, oy, bw | bh << 16, first list entry)
     uint64_t seed;
+    float *var;               // per-pixel sample statistics W x H x 8 (sum L, sum L^2, n) or null
 };
 
 // stack = LDS stack depth (8, 16, 32 or 64) chosen from the BVH depth.

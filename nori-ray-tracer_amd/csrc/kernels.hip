@@ -1558,10 +1558,21 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
 // ImageBlock::put(pos, val) (block.cpp:93-122) of one sample straight into
 // the film, with the block-relative coordinates of the sample's own block so
 // the filter weights round exactly as in k_splat.
-ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, uint32_t y, V2 jit, float4 L) {
+ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, uint32_t y, V2 jit, float4 L,
+                     float *var) {
     if (L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z)) {
         atomicAdd(&C->invalid, 1ull);
         return;
+    }
+    if (var) {  // the pixel's sample statistics (nori_gpu_render_desc.variance_out)
+        float *v = var + 8 * ((size_t)y * S.W + x);
+        atomicAdd(v + 0, L.x);
+        atomicAdd(v + 1, L.y);
+        atomicAdd(v + 2, L.z);
+        atomicAdd(v + 3, L.x * L.x);
+        atomicAdd(v + 4, L.y * L.y);
+        atomicAdd(v + 5, L.z * L.z);
+        atomicAdd(v + 6, 1.0f);
     }
     const int B = S.border, TS = NORI_BLOCK_SIZE + 2 * B, FW = S.W + 2 * B;
     const int ox = (int)(x / NORI_BLOCK_SIZE) * NORI_BLOCK_SIZE, oy = (int)(y / NORI_BLOCK_SIZE) * NORI_BLOCK_SIZE;
@@ -1788,7 +1799,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             wave_seed(rg, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
             V2 jit = next2D(rg);
             // Sg: kernarg filter table (no local copy)
-            splat_sample(Sg, film, C, x, y, jit, make_float4(ps.L.x, ps.L.y, ps.L.z, 0.0f));
+            splat_sample(Sg, film, C, x, y, jit, make_float4(ps.L.x, ps.L.y, ps.L.z, 0.0f), wd.var);
             atomicAdd(&seg.stats[sg].w, rays);
             atomicAdd(&C->finish_paths, 1u);
             atomicMax(&C->finish_max_rays, rays);
@@ -1996,6 +2007,7 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
 #pragma unroll
             for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = acc[a][c][2] = acc[a][c][3] = 0.0f;
         bool any = false;
+        float vs[7] = {0, 0, 0, 0, 0, 0, 0};  // sample statistics of the pixel (sd.var)
         // the next pass's record is in flight while this one is splatted
         float4 Ln = p0 < p1 ? rec[(size_t)p0 * sd.M + off + j] : make_float4(0, 0, 0, 1);
         for (uint32_t p = p0; p < p1; ++p) {
@@ -2013,6 +2025,13 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
                 continue;
             }
             any = true;
+            vs[0] += L.x;
+            vs[1] += L.y;
+            vs[2] += L.z;
+            vs[3] += L.x * L.x;
+            vs[4] += L.y * L.y;
+            vs[5] += L.z * L.z;
+            vs[6] += 1.0f;
             float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
             int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
             int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
@@ -2042,6 +2061,10 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
                     acc[a][c][2] += lz_[c] * wy[a];
                     acc[a][c][3] += wx[c] * wy[a];  // (1 * wx) * wy
                 }
+        }
+        if (any && sd.var) {
+            float *v = sd.var + 8 * ((size_t)y * S.W + x);
+            for (int k = 0; k < 7; ++k) atomicAdd(v + k, vs[k]);
         }
         if (any) {
 #pragma unroll

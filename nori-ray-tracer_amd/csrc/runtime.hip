@@ -200,6 +200,7 @@ struct nori_gpu_ctx {
     // render state
     DevBuf q[2][6], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
     DevBuf ptctr;                    // persistent traversal work counters, 4 per part
+    DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
     uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
@@ -667,6 +668,25 @@ void setup_persistent(nori_gpu_ctx &c) {
     HIP_TRY(hipMemset(c.ptctr.p, 0, 4 * 4 * kMaxParts));
 }
 
+// Per-pixel sample statistics (render_desc.variance_out): the device buffer
+// the kernels add into -- the caller's own when it is device memory, else a
+// zeroed scratch buffer that var_finish adds into the host array.
+float *var_begin(nori_gpu_ctx &c, const nori_gpu_render_desc &rd) {
+    if (!rd.variance_out) return nullptr;
+    if (rd.output_on_device) return rd.variance_out;
+    const size_t n = 8 * (size_t)c.S.W * (size_t)c.S.H;
+    c.varbuf.ensure(n * sizeof(float));
+    HIP_TRY(hipMemsetAsync(c.varbuf.p, 0, n * sizeof(float), c.stream));
+    return c.varbuf.as<float>();
+}
+void var_finish(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, bool cancelled) {
+    if (!rd.variance_out || rd.output_on_device || cancelled) return;
+    const size_t n = 8 * (size_t)c.S.W * (size_t)c.S.H;
+    std::vector<float> h(n);
+    HIP_TRY(hipMemcpy(h.data(), c.varbuf.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; ++i) rd.variance_out[i] += h[i];
+}
+
 // normals / av / direct*: no path pool -- per chunk of passes, k_direct runs
 // every sample start to end and writes its record, then k_splat filters them.
 int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std::vector<uint32_t> &pixels,
@@ -701,15 +721,16 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
     std::vector<std::array<hipEvent_t, 3>> spans;
     uint64_t done = 0;
     bool cancelled = false;
+    float *var = var_begin(c, rd);
     for (uint32_t p0 = 0; p0 < passes; p0 += chunk) {
         if (c.cancel.load()) {
             cancelled = true;
             break;
         }
         const uint32_t np = std::min(chunk, passes - p0);
-        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, 0, nullptr, 1, 0};
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, 0, nullptr, 1, 0, var};
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)), c.blocks.as<int4>(),
-                     rd.seed};
+                     rd.seed, var};
         std::array<hipEvent_t, 3> ev{};
         if (timing) {
             for (auto &e : ev) e = tm.get();
@@ -741,6 +762,7 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
         HIP_TRY(hipMemcpy(hf.data(), film, film_elems * sizeof(float), hipMemcpyDeviceToHost));
         for (size_t i = 0; i < film_elems; ++i) rgbw_out[i] += hf[i];
     }
+    var_finish(c, rd, cancelled);
     c.progress = 1.0f;
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -872,9 +894,11 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                  c.segstats.as<uint4>()};
     std::vector<uint4> hstats(G);
     uint64_t finish_rays = 0, samples_started = 0;
+    float *var = var_begin(c, rd);
     for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
         uint32_t np = std::min(chunk, passes - p0);
-        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev, 1, 0};
+        WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev, 1, 0,
+                    var};
         wd.rot = stream_rotation(wd.total, M, G);
         __atomic_store_n(&c.pinned[0], 0u, __ATOMIC_RELEASE);
         __atomic_store_n(&c.pinned[1], 0u, __ATOMIC_RELEASE);
@@ -979,7 +1003,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipEventRecord(c.fork, c.stream));
         HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)),
-                     c.blocks.as<int4>(), rd.seed};
+                     c.blocks.as<int4>(), rd.seed, var};
         timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
         timed(4, [&] {
             return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack, c.tailpre.as<uint32_t>(), c.stream);
@@ -1030,6 +1054,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipMemcpy(hf.data(), film, film_elems * sizeof(float), hipMemcpyDeviceToHost));
         for (size_t i = 0; i < film_elems; ++i) rgbw_out[i] += hf[i];
     }
+    var_finish(c, rd, cancelled);
     HIP_TRY(hipStreamSynchronize(c.stream));
     HIP_TRY(hipStreamSynchronize(c.side));
     for (int h = 1; h < kMaxParts; ++h) HIP_TRY(hipStreamSynchronize(c.parts[h]));

@@ -25,7 +25,7 @@ from . import _abi
 from ._abi import NoriError, check, lib  # noqa: F401
 
 __all__ = ["load_scene", "Scene", "GpuRenderer", "RenderThread", "NoriError", "device_count",
-           "develop", "write_exr"]
+           "develop", "write_exr", "write_png", "read_exr", "film_variance"]
 
 
 def _fptr(a):
@@ -127,6 +127,23 @@ def write_exr(path, rgb):
     check(lib().nori_write_exr(os.fsencode(path), _fptr(rgb), rgb.shape[1], rgb.shape[0]))
 
 
+def write_png(path, rgb):
+    """Bitmap::saveToLDR (bitmap.cpp:109-139): sRGB curve, 8-bit RGB PNG."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    check(lib().nori_write_png(os.fsencode(path), _fptr(rgb), rgb.shape[1], rgb.shape[0]))
+
+
+def film_variance(scene, stats):
+    """Variance of each pixel's mean (H, W, 3) from the (H, W, 8) sample
+    statistics GpuRenderer.render(variance=...) accumulates (nori_film_variance)."""
+    stats = np.ascontiguousarray(stats, dtype=np.float32)
+    if stats.shape != (scene.height, scene.width, 8):
+        raise ValueError(f"statistics shape {stats.shape} != {(scene.height, scene.width, 8)}")
+    out = np.zeros((scene.height, scene.width, 3), np.float32)
+    check(lib().nori_film_variance(scene.desc_ptr, _fptr(stats), _fptr(out)))
+    return out
+
+
 class BvhInfo(C.Structure):
     _fields_ = [("ref_nodes", C.c_uint32), ("device_nodes", C.c_uint32), ("depth", C.c_uint32),
                 ("num_prims", C.c_uint32), ("sah_cost", C.c_float), ("pad", C.c_uint32), ("order_hash", C.c_uint64)]
@@ -177,12 +194,15 @@ class GpuRenderer:
         self.close()
 
     def render(self, passes=None, pass_begin=0, blocks=None, seed=0, out=None, path_pool=0,
-               device_ptr=None, timing=False):
+               device_ptr=None, timing=False, variance=None):
         """Render passes [pass_begin, pass_begin+passes) of `blocks` (all if None).
 
         Returns the RGBW film (H+2b, W+2b, 4) as float32, accumulated into
         `out` when given.  With `device_ptr` (an int device address, e.g. a
         torch tensor's data_ptr()) the film is accumulated on the GPU instead.
+        `variance`: an (H, W, 8) float32 array (host mode) or an int device
+        address (device mode) that the per-pixel sample statistics are added
+        into (see film_variance).
         """
         rd = _abi.RenderDesc()
         rd.pass_begin = int(pass_begin)
@@ -195,6 +215,13 @@ class GpuRenderer:
         rd.seed = int(seed)
         rd.path_pool = int(path_pool)
         rd.timing = int(bool(timing))
+        if variance is not None:
+            if device_ptr is not None:
+                rd.variance_out = int(variance)
+            else:
+                assert (isinstance(variance, np.ndarray) and variance.dtype == np.float32 and variance.flags.c_contiguous
+                        and variance.shape == (self.scene.height, self.scene.width, 8))
+                rd.variance_out = variance.ctypes.data
         st = _abi.Stats()
         if device_ptr is not None:
             rd.output_on_device = 1
@@ -234,8 +261,11 @@ class RenderThread:
         self._status = 0  # 0 idle, 1 rendering, 2 stop requested, 3 done
         self.error = None
         self.image = None
+        self.variance = None
 
     def renderScene(self, filename, width=0, height=0, spp=0):
+        """Writes <stem>.exr and <stem>_variance.exr (render.cpp:158-169, 256-276;
+        the variance image is the variance of each pixel's mean, deviation D5)."""
         scene = load_scene(filename, width, height, spp)
         stem = os.path.splitext(filename)[0]
 
@@ -244,10 +274,13 @@ class RenderThread:
                 self._renderer = GpuRenderer(scene, self.device)
                 t0 = time.time()
                 print("Rendering .. ", end="", flush=True)
-                film = self._renderer.render()
+                stats = np.zeros((scene.height, scene.width, 8), np.float32)
+                film = self._renderer.render(variance=stats)
                 print(f"done. (took {1e3 * (time.time() - t0):.1f}ms)")
                 self.image = develop(scene, film)
                 write_exr(stem + ".exr", self.image)
+                self.variance = film_variance(scene, stats)
+                write_exr(stem + "_variance.exr", self.variance)
             except NoriError as e:
                 self.error = e
             finally:

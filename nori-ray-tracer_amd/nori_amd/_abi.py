@@ -1,4 +1,4 @@
-"""ctypes mirror of include/nori_gpu.h (ABI version 2).
+"""ctypes mirror of include/nori_gpu.h (ABI version 3).
 
 The structures below must match the C declarations field for field; the
 test suite checks their sizes against the library (tests/test_abi.py).
@@ -6,7 +6,7 @@ test suite checks their sizes against the library (tests/test_abi.py).
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 NORI_OK = 0
 NORI_ERR_INVALID = -1
@@ -85,7 +85,8 @@ class SceneDesc(C.Structure):
 class RenderDesc(C.Structure):
     _fields_ = [("pass_begin", C.c_uint32), ("pass_count", C.c_uint32), ("num_blocks", C.c_uint32),
                 ("block_ids", C.POINTER(C.c_uint32)), ("seed", C.c_uint64),
-                ("output_on_device", C.c_int32), ("path_pool", C.c_uint32), ("timing", C.c_int32)]
+                ("output_on_device", C.c_int32), ("path_pool", C.c_uint32), ("timing", C.c_int32),
+                ("variance_out", C.c_void_p)]
 
 
 class Stats(C.Structure):
@@ -116,6 +117,8 @@ SIGNATURES = {
     "nori_filter_table": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_float)]),
     "nori_film_develop": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "nori_write_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, C.c_int]),
+    "nori_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, C.c_int]),
+    "nori_film_variance": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "nori_read_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)]),
     "nori_scene_bvh_info": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nori_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
