@@ -151,8 +151,11 @@ def roofline(ts, samples):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    # default warm-up: 2 renders -- the first render after a context's first
+    # render runs ~17 ms (~40 %) longer with identical kernel times
+    # (tools/step_times.py); from the third on the step time is steady
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--spp", type=int, default=512)

@@ -72,7 +72,7 @@ ND bool tri_hit(const float4 &a, const float4 &b, const float4 &c, const TRay &r
     V3 pvec = cross(r.d, e2);
     float det = dot(e1, pvec);
     if (det > -1e-8f && det < 1e-8f) return false;
-    float inv_det = 1.0f / det;
+    float inv_det = rcp_rn(det);  // == 1.0f / det (tools/rcp_check.hip)
     V3 tvec = r.o - v0;
     u = dot(tvec, pvec) * inv_det;
     if (u < 0.0f || u > 1.0f) return false;
@@ -107,7 +107,7 @@ ND bool tri_hit_nb(const float4 &a, const float4 &b, const float4 &c, const TRay
     V3 v0 = ld3(a), e1 = ld3(b), e2 = ld3(c);
     V3 pvec = cross(r.d, e2);
     float det = dot(e1, pvec);
-    float inv_det = 1.0f / det;
+    float inv_det = rcp_rn(det);  // == 1.0f / det (tools/rcp_check.hip)
     V3 tvec = r.o - v0;
     u = dot(tvec, pvec) * inv_det;
     V3 qvec = cross(tvec, e1);
@@ -816,15 +816,21 @@ ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, 
     SurfHit h;
     h.shape = (int)S.prim_shape[prim];
     const DevShape &sh = S.shapes[h.shape];
+    // only a textured albedo reads the texture coordinates (BRec.uv): the
+    // sphere's atan2/acos are skipped for every other BSDF
+    const bool need_uv = S.bsdfs[sh.bsdf].tex != NORI_TEXTURE_CONSTANT;
+    h.uv = V2{u, v};
     if (sh.type == NORI_SHAPE_SPHERE) {
         h.p = o + d * t;
         const V3 n = normalize(h.p - V3{sh.center[0], sh.center[1], sh.center[2]});
         h.sh = frame_from(n);
-        // sphericalCoordinates (common.cpp:264-272); 0.5 is a double literal
-        float phi = atan2f(n.y, n.x);
-        if (phi < 0) phi += 2 * kPi;
-        h.uv.x = (float)(0.5 + (double)(acosf(n.z) / (2 * kPi)));
-        h.uv.y = phi / kPi;
+        if (need_uv) {
+            // sphericalCoordinates (common.cpp:264-272); 0.5 is a double literal
+            float phi = atan2f(n.y, n.x);
+            if (phi < 0) phi += 2 * kPi;
+            h.uv.x = (float)(0.5 + (double)(acosf(n.z) / (2 * kPi)));
+            h.uv.y = phi / kPi;
+        }
     } else {
         const uint32_t *f = S.tri_vidx + 3 * (size_t)prim;
         uint32_t i0 = f[0], i1 = f[1], i2 = f[2];
@@ -832,8 +838,7 @@ ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, 
         V3 p0 = ld3(q0), p1 = ld3(q1), p2 = ld3(q2);
         float bx = 1 - (u + v);
         h.p = (p0 * bx + p1 * u) + p2 * v;
-        h.uv = V2{u, v};
-        if (sh.has_uvs)  // u in pos.w, v in nrm.w
+        if (need_uv && sh.has_uvs)  // u in pos.w, v in nrm.w
             h.uv = V2{(bx * q0.w + u * q1.w) + v * q2.w,
                       (bx * S.nrm[i0].w + u * S.nrm[i1].w) + v * S.nrm[i2].w};
         if (sh.has_normals) {

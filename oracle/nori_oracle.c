@@ -1975,7 +1975,8 @@ int oracle_bsdf_sample(const nori_bsdf_desc *bd, const float *wi, const float *u
 int oracle_bsdf_eval_pdf(const nori_bsdf_desc *bd, const float *wi, const float *wo, uint32_t n, float *out) {
     Bsdf b; bsdf_init(&b, bd);
     for (uint32_t i = 0; i < n; ++i) {
-        BRec br; br.wi = v3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]); br.wo = v3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
+        BRec br; memset(&br, 0, sizeof(br));
+        br.wi = v3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]); br.wo = v3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
         br.measure = M_SOLID_ANGLE; br.eta = 1.0f;
         V3 f = bsdf_eval(&b, &br);
         float *o = out + 4 * (size_t)i;
