@@ -36,8 +36,8 @@ def _gpu_vs_oracle(s):
     return gpu, cpu, l2, exact, st
 
 
-SCENES = ["pa1/sphere-analytic.xml", "pa1/sphere-mesh.xml", "pa1/sphere-texture.xml", "pa3/sphere/point_ems.xml",
-          "pa3/sphere/sphere_ems.xml", "pa3/sphere/sphere_mats.xml", "pa3/sphere/sphere_mesh_ems.xml",
+SCENES = ["pa1/sphere-analytic.xml", "pa1/sphere-mesh.xml", "pa1/sphere-texture.xml", "pa1/mesh-texture.xml",
+          "pa3/sphere/point_ems.xml", "pa3/sphere/sphere_ems.xml", "pa3/sphere/sphere_mats.xml", "pa3/sphere/sphere_mesh_ems.xml",
           "pa3/odyssey/odyssey_ems.xml", "pa3/odyssey/odyssey_mats.xml", "pa3/odyssey/odyssey_mis.xml",
           "pa3/veach_mi/veach_mis.xml", "project/spotlight/sphere-texture.xml"]
 
@@ -55,7 +55,8 @@ def test_one_bounce_matches_oracle(built, xml):
 @pytest.mark.parametrize("xml,golden", [("pa3/sphere/sphere_ems.xml", "pa3/sphere/ref/sphere_ems.exr"),
                                         ("pa3/odyssey/odyssey_mis.xml", "pa3/odyssey/ref/odyssey_mis_32spp.exr"),
                                         ("pa3/veach_mi/veach_mis.xml", "pa3/veach_mi/ref/veach_mis_128spp.exr"),
-                                        ("pa1/sphere-texture.xml", "pa1/ref/sphere-texture.exr")])
+                                        ("pa1/sphere-texture.xml", "pa1/ref/sphere-texture.exr"),
+                                        ("pa1/mesh-texture.xml", "pa1/ref/mesh-texture.exr")])
 def test_one_bounce_full_size_matches_golden(built, xml, golden):
     s = nori_amd.load_scene(scene_path(xml))
     with nori_amd.GpuRenderer(s, 0) as r:

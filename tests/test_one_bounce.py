@@ -6,8 +6,8 @@ ray generators.  No GPU needed.
 Fixtures (all from the reference's own scene tree, copied as data):
 * Student-t tests scenes/pa1/test-av.xml and scenes/pa1/test-direct.xml
   (ttest.cpp:147-194; references 0.894/0.707/0.707/1 and 1/0.06317/0/1.06317).
-* golden renders of the course solution: scenes/pa1/ref/sphere-{analytic,mesh,
-  texture}.exr, scenes/pa3/sphere/ref/*.exr, scenes/pa3/odyssey/ref/*.exr,
+* golden renders of the course solution: scenes/pa1/ref/{sphere-analytic,sphere-mesh,
+  sphere-texture,mesh-texture}.exr, scenes/pa3/sphere/ref/*.exr, scenes/pa3/odyssey/ref/*.exr,
   scenes/pa3/veach_mi/ref/veach_mis_128spp.exr.  Compared in expectation: the
   oracle at a few spp against the golden at its own spp, by channel means and
   16x16-block relMSE.  Measured (block stream, 8 threads): channel means within
@@ -54,6 +54,7 @@ GOLDEN_CASES = [
     ("pa1/sphere-analytic.xml", "pa1/ref/sphere-analytic.exr", 4, 2e-3, 1e-4),
     ("pa1/sphere-mesh.xml", "pa1/ref/sphere-mesh.exr", 4, 2e-3, 1e-4),
     ("pa1/sphere-texture.xml", "pa1/ref/sphere-texture.exr", 4, 2e-3, 1e-4),
+    ("pa1/mesh-texture.xml", "pa1/ref/mesh-texture.exr", 4, 2e-3, 1e-4),  # mesh UVs (camelhead.obj)
     ("pa3/sphere/point_ems.xml", "pa3/sphere/ref/point_ems.exr", 4, 2e-3, 1e-5),
     ("pa3/sphere/sphere_ems.xml", "pa3/sphere/ref/sphere_ems.exr", 16, 5e-3, 2e-3),
     ("pa3/sphere/sphere_mats.xml", "pa3/sphere/ref/sphere_mats.exr", 16, 5e-3, 4e-3),
