@@ -1981,6 +1981,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_direct(DevScene S, WorkDesc wd,
 }
 
 // ------------------------------------------------------------------ film splat
+#ifndef NORI_SPLAT_DEPTH
+#define NORI_SPLAT_DEPTH 1  // sample records in flight per thread (prefetch depth)
+#endif
 // ImageBlock::put(pos, val) (block.cpp:93-122) for every sample of one 32x32
 // block and a range of passes, then ImageBlock::put(block) (block.cpp:124-133)
 // into the film.  A thread owns one pixel: all samples of that pixel fall in
@@ -2013,11 +2016,16 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
             for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = acc[a][c][2] = acc[a][c][3] = 0.0f;
         bool any = false;
         float vs[7] = {0, 0, 0, 0, 0, 0, 0};  // sample statistics of the pixel (sd.var)
-        // the next pass's record is in flight while this one is splatted
-        float4 Ln = p0 < p1 ? rec[(size_t)p0 * sd.M + off + j] : make_float4(0, 0, 0, 1);
+        // the next NORI_SPLAT_DEPTH passes' records are in flight while this one is splatted
+        float4 Lq[NORI_SPLAT_DEPTH];
+#pragma unroll
+        for (int d = 0; d < NORI_SPLAT_DEPTH; ++d)
+            Lq[d] = p0 + d < p1 ? rec[(size_t)(p0 + d) * sd.M + off + j] : make_float4(0, 0, 0, 1);
         for (uint32_t p = p0; p < p1; ++p) {
-            const float4 L = Ln;
-            if (p + 1 < p1) Ln = rec[(size_t)(p + 1) * sd.M + off + j];
+            const float4 L = Lq[0];
+#pragma unroll
+            for (int d = 0; d + 1 < NORI_SPLAT_DEPTH; ++d) Lq[d] = Lq[d + 1];
+            if (p + NORI_SPLAT_DEPTH < p1) Lq[NORI_SPLAT_DEPTH - 1] = rec[(size_t)(p + NORI_SPLAT_DEPTH) * sd.M + off + j];
             if (L.w != 0.0f) continue;  // pending: the finisher splats this sample
             uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
             Pcg r;

@@ -641,6 +641,19 @@ bool fused_extend() {
     const char *e = std::getenv("NORI_FUSED_EXTEND");
     return e && e[0] == '1';
 }
+// Sample passes folded by one splat work-group.  Default: about one
+// work-group per CU over the whole launch (passes x blocks / 256), so the
+// splat leaves most of the chip to the tail finisher it overlaps with
+// (cbox 512x512@512: 256 blocks x 512 passes per work-group, splat 3.0 ms and
+// finisher 3.6 ms vs 4.7 / 5.2 ms at 32 passes).  NORI_SPLAT_PASSES overrides.
+// The one-bounce integrators' splat has no finisher beside it: it targets
+// 4096 work-groups instead.
+uint32_t splat_passes(uint32_t np, size_t nblocks, uint32_t target_wgs = 256) {
+    const char *e = std::getenv("NORI_SPLAT_PASSES");
+    long v = e ? std::atol(e) : (long)(((uint64_t)np * nblocks + target_wgs - 1) / target_wgs);
+    if (v < 1) v = 1;
+    return (uint32_t)std::min<long>(v, np);
+}
 bool overlap_splat() {
     const char *e = std::getenv("NORI_SPLAT_OVERLAP");
     return !(e && e[0] == '0');
@@ -729,7 +742,7 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
         }
         const uint32_t np = std::min(chunk, passes - p0);
         WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, 0, nullptr, 1, 0, var};
-        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)), c.blocks.as<int4>(),
+        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, splat_passes(np, blocks.size(), 4096)), c.blocks.as<int4>(),
                      rd.seed, var};
         std::array<hipEvent_t, 3> ev{};
         if (timing) {
@@ -1002,7 +1015,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(launch_mark(Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stream));
         HIP_TRY(hipEventRecord(c.fork, c.stream));
         HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));
-        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, std::min<uint32_t>(np, 32)),
+        SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, splat_passes(np, blocks.size())),
                      c.blocks.as<int4>(), rd.seed, var};
         timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
         timed(4, [&] {
