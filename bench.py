@@ -15,7 +15,9 @@ Extra fields:
   roofline     -- the dominant kernel (most HIP-event time in the last timed
                   step; k_shade on this workload): algorithmic HBM bytes per
                   launch over its average launch time against the 8 TB/s HBM
-                  peak, `traffic` = measured HBM bytes per launch from the
+                  peak (launch times inside the timed region, where two pool
+                  parts on two streams share the chip; `isolated_frac` uses the
+                  serialised launch time of the committed counter passes), `traffic` = measured HBM bytes per launch from the
                   committed rocprofv3 PMC summary (profiles/pmc_r01.json), and
                   a per-kernel table (the traversal kernels are VALU-bound:
                   VALU issue rate against the issue peak).
@@ -135,6 +137,12 @@ def roofline(ts, samples):
         if prof:
             row["traffic_bytes_per_launch"] = prof.get("hbm_bytes_per_launch")
             row["rocprof_avg_launch_ms"] = prof.get("trace_avg_ms")
+            # the counter passes serialise the kernels: this launch time has no
+            # second stream beside it (the timed region overlaps two pool parts)
+            iso = prof.get("profiled_ms_per_launch")
+            if iso:
+                row["isolated_launch_ms"] = iso
+                row["isolated_achieved_GBs"] = nbytes / launches / (iso / 1e3) / 1e9
             if prof.get("sq_insts_valu_per_launch") and prof.get("trace_avg_ms"):
                 rate = prof["sq_insts_valu_per_launch"] * 64 / (prof["trace_avg_ms"] / 1e3)
                 row["valu_lane_instr_per_s"] = rate
@@ -144,6 +152,7 @@ def roofline(ts, samples):
     d = rows[dom]
     return {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": d["achieved_GBs"] / HBM_PEAK_GBS, "traffic": d.get("traffic_bytes_per_launch"),
+            "isolated_frac": (d["isolated_achieved_GBs"] / HBM_PEAK_GBS) if "isolated_achieved_GBs" in d else None,
             "bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": d["avg_launch_ms"], "launches": launches,
             "kernels": rows}
 
