@@ -66,6 +66,49 @@ ND bool box_test(const float4 &mn, const float4 &mx, const TRay &r, float &tnear
     return ok && r.mint <= farT && nearT <= r.maxt;
 }
 
+// One 4-wide BVH node: the child boxes in SoA form (mnx.x = child 0's min.x,
+// ...) and the four child references.  NORI_BVH_QUANT: a 64-byte quantized
+// node (bvh_builder.cpp quantize_nodes) decoded as origin + (float)q * s --
+// the builder checked with this same arithmetic that every decoded box
+// contains the exact one; an unused child (q_lo > q_hi) gets a NaN box, which
+// box_test never enters.  Otherwise the exact 128-byte node.
+#if NORI_BVH_QUANT
+ND float qdec(float o, uint32_t w, int i, float s) { return o + (float)((w >> (8 * i)) & 0xFFu) * s; }
+#endif
+ND void load_node(const DevScene &S, uint32_t ref, float4 &mnx, float4 &mny, float4 &mnz, float4 &mxx, float4 &mxy,
+                  float4 &mxz, float4 &rf) {
+#if NORI_BVH_QUANT
+    const float4 *nd = S.nodes + 4 * (size_t)ref;
+    const float4 a = gld(nd), b = gld(nd + 1), c = gld(nd + 2);
+    rf = gld(nd + 3);
+    const uint32_t lx = __float_as_uint(b.z), ly = __float_as_uint(b.w), lz = __float_as_uint(c.x);
+    const uint32_t hx = __float_as_uint(c.y), hy = __float_as_uint(c.z), hz = __float_as_uint(c.w);
+    const float sx = a.w, sy = b.x, sz = b.y;
+    float v[6][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[0][i] = qdec(a.x, lx, i, sx);
+        v[1][i] = qdec(a.y, ly, i, sy);
+        v[2][i] = qdec(a.z, lz, i, sz);
+        v[3][i] = qdec(a.x, hx, i, sx);
+        v[4][i] = qdec(a.y, hy, i, sy);
+        v[5][i] = qdec(a.z, hz, i, sz);
+        if (!(v[0][i] <= v[3][i]))  // unused child: NaN box (every axis with d != 0 rejects it)
+            v[0][i] = v[1][i] = v[2][i] = v[3][i] = v[4][i] = v[5][i] = __builtin_nanf("");
+    }
+    mnx = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]);
+    mny = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
+    mnz = make_float4(v[2][0], v[2][1], v[2][2], v[2][3]);
+    mxx = make_float4(v[3][0], v[3][1], v[3][2], v[3][3]);
+    mxy = make_float4(v[4][0], v[4][1], v[4][2], v[4][3]);
+    mxz = make_float4(v[5][0], v[5][1], v[5][2], v[5][3]);
+#else
+    const float4 *nd = S.nodes + 8 * (size_t)ref;
+    mnx = gld(nd), mny = gld(nd + 1), mnz = gld(nd + 2), mxx = gld(nd + 3), mxy = gld(nd + 4), mxz = gld(nd + 5);
+    rf = gld(nd + 6);
+#endif
+}
+
 // Mesh::rayIntersect (mesh.cpp:83-120), edges precomputed exactly.
 ND bool tri_hit(const float4 &a, const float4 &b, const float4 &c, const TRay &r, float &t, float &u, float &v) {
     V3 v0 = ld3(a), e1 = ld3(b), e2 = ld3(c);
@@ -268,9 +311,8 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     bool found = false;
     for (;;) {
         if (!(ref & 0x80000000u)) {
-            const float4 *nd = S.nodes + 8 * (size_t)ref;
-            const float4 mnx = gld(nd), mny = gld(nd + 1), mnz = gld(nd + 2), mxx = gld(nd + 3), mxy = gld(nd + 4),
-                         mxz = gld(nd + 5), rf = gld(nd + 6);
+            float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
+            load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
             float k0, k1, k2, k3;
             bool h;
             h = box_test(make_float4(mnx.x, mny.x, mnz.x, 0), make_float4(mxx.x, mxy.x, mxz.x, 0), r, k0);
@@ -604,9 +646,8 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(Dev
             if (!__any(in_node)) break;
             if (NORI_PT_SPEC ? __all(!active || has_leaf || !has_ref) : __any(active && has_leaf)) break;
             if (in_node) {
-                const float4 *nd = S.nodes + 8 * (size_t)ref;
-                const float4 mnx = gld(nd), mny = gld(nd + 1), mnz = gld(nd + 2), mxx = gld(nd + 3),
-                             mxy = gld(nd + 4), mxz = gld(nd + 5), rf = gld(nd + 6);
+                float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
+                load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
                 float k0, k1, k2, k3;
                 const bool h0 = box_test(make_float4(mnx.x, mny.x, mnz.x, 0), make_float4(mxx.x, mxy.x, mxz.x, 0), r, k0);
                 const bool h1 = box_test(make_float4(mnx.y, mny.y, mnz.y, 0), make_float4(mxx.y, mxy.y, mxz.y, 0), r, k1);
