@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define NORI_GPU_ABI_VERSION 3
+#define NORI_GPU_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define NORI_OK               0
@@ -85,7 +85,8 @@ enum {
     NORI_INTEGRATOR_DIRECT = 5,     /* "direct"      src/direct.cpp            */
     NORI_INTEGRATOR_DIRECT_EMS = 6, /* "direct_ems"  src/direct_ems.cpp        */
     NORI_INTEGRATOR_DIRECT_MATS = 7,/* "direct_mats" src/direct_mats.cpp       */
-    NORI_INTEGRATOR_DIRECT_MIS = 8  /* "direct_mis"  src/direct_mis.cpp        */
+    NORI_INTEGRATOR_DIRECT_MIS = 8, /* "direct_mis"  src/direct_mis.cpp        */
+    NORI_INTEGRATOR_PHOTONMAPPER = 9 /* "photonmapper" src/photonmapper.cpp    */
 };
 enum {
     NORI_FILTER_GAUSSIAN = 0, NORI_FILTER_MITCHELL = 1, NORI_FILTER_TENT = 2,
@@ -188,6 +189,9 @@ typedef struct nori_scene_desc {
     int32_t integrator;           /* NORI_INTEGRATOR_*                          */
     uint32_t sample_count;        /* independent sampler sampleCount = spp      */
     float av_length;              /* "av" integrator ray length                 */
+    uint32_t photon_count;        /* photonmapper "photonCount" (photons stored) */
+    float photon_radius;          /* photonmapper "photonRadius" (0 in the XML:
+                                     scene box diagonal / 500, photonmapper.cpp:55-56) */
 } nori_scene_desc;
 
 /* ---- host-side scene loading (the plugin boundary) ----------------------- */

@@ -85,11 +85,26 @@ struct DevScene {
     float sigma_t[3], albedo[3];
     // Small scenes: every table above packed into one blob (byte offsets),
     // which latency-bound kernels stage into LDS (blob_bytes == 0: none).
+    // photonmapper: photons (position, direction, power; 3 float4 each) sorted
+    // by hash-grid bucket, bucket starts (ph_mask + 2 entries), cell size r
+    const float4 *ph;
+    const uint32_t *ph_start;
+    uint32_t ph_mask;
+    float ph_inv_cell, ph_r2, ph_norm;  // 1/r, r*r, r*r*photonCount (photonmapper.cpp:177)
     const float4 *blob;
     uint32_t blob_bytes;
     uint32_t off_prims, off_vidx, off_pos, off_nrm, off_pshape, off_shapes, off_bsdfs, off_emitters, off_cdf,
         off_nodes;
 };
+
+// Photon-map hash grid: integer cell -> bucket (masked by the caller).
+NHD uint32_t photon_cell_hash(int x, int y, int z) {
+    return ((uint32_t)x * 73856093u) ^ ((uint32_t)y * 19349663u) ^ ((uint32_t)z * 83492791u);
+}
+// Stream seed of the photon-tracing pass: photon e draws from pcg32 stream
+// wave_seed(kPhotonSeed, e) (deviation D8; the reference draws every photon
+// from one unseeded sampler in sequence, photonmapper.cpp:47-48).
+constexpr uint64_t kPhotonSeed = 0x70686f746f6e6d70ull;
 
 // A copy of S whose small-scene tables point into `lds` (the staged blob).
 ND DevScene scene_in_lds(const DevScene &S, const char *lds) {

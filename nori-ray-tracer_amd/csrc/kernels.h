@@ -58,8 +58,6 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                          hipStream_t st);
-// One-bounce integrators (normals, av, direct, direct_ems/mats/mis): one thread
-// per work id of wd (pass-major, pixels in wd.pixels order) writes its record.
 // Persistent BVH traversal (k_trace_pt): `blocks` resident work-groups pull
 // queue segments through ctr[0..1] (zero before the first launch; each launch
 // leaves them zero).  Stacks 8, 16, 32 only (BVH scenes).
@@ -68,6 +66,15 @@ hipError_t launch_extend_pt(const DevScene &S, const PathQueue &q, const uint32_
 hipError_t launch_shadow_pt(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                             int stack, uint32_t *ctr, uint32_t blocks, hipStream_t st);
 int pt_blocks_per_cu(int stack, bool any);
+// Photon tracing (photonmapper preprocess): count pass (out == null) writes
+// the photons stored by each emitted photon e0 + i into count[i]; store pass
+// writes the photons of emitted photons i < n at pre[i] (3 float4 each:
+// position, direction towards the light, power), `total` photons in all.
+hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *count, const uint64_t *pre,
+                          uint64_t total, float4 *out, int stack, hipStream_t st);
+// One-bounce integrators (normals, av, direct, direct_ems/mats/mis) and the
+// photon mapper: one thread per work id of wd (pass-major, pixels in
+// wd.pixels order) writes its record.
 hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack, hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);

@@ -1903,8 +1903,67 @@ struct OneBounce {
         if (sh.emitter < 0) return V3{0, 0, 0};
         return emitter_eval(S, S.emitters[sh.emitter], hs.sh.n, normalize(hs.p - from));
     }
+    // PhotonMapper::Li (photonmapper.cpp:119-196): emission at every hit, the
+    // photon density estimate at the first diffuse surface, Russian roulette
+    // and BSDF sampling at the others.  The kd-tree search (kdtree.h:260-316:
+    // every photon with |x - p|^2 < r^2) is a 27-cell lookup in a hash grid of
+    // cell size r: a bucket may hold photons of colliding cells, so each
+    // photon is counted only from its own cell.
+    ND V3 Li_pmap(Pcg &rng, V3 o, V3 d, float mint, float maxt) {
+        V3 color{0, 0, 0}, att{1, 1, 1};
+        for (;;) {
+            SurfHit hs;
+            if (!closest(o, d, mint, maxt, hs)) return color;
+            color = color + att * emission(hs, o);
+            const DevBsdf &B = S.bsdfs[S.shapes[hs.shape].bsdf];
+            if (B.type == NORI_BSDF_DIFFUSE) {  // Diffuse::isDiffuse (diffuse.cpp:122)
+                const float ic = S.ph_inv_cell;
+                const int cx = (int)floorf(hs.p.x * ic), cy = (int)floorf(hs.p.y * ic), cz = (int)floorf(hs.p.z * ic);
+                const V3 wi = to_local(hs.sh, -d);
+                V3 pc{0, 0, 0};
+                for (int dz = -1; dz <= 1; ++dz)
+                    for (int dy = -1; dy <= 1; ++dy)
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            const int gx = cx + dx, gy = cy + dy, gz = cz + dz;
+                            const uint32_t h = photon_cell_hash(gx, gy, gz) & S.ph_mask;
+                            const uint32_t j1 = S.ph_start[h + 1];
+                            for (uint32_t j = S.ph_start[h]; j < j1; ++j) {
+                                const float4 pp = gld(S.ph + 3 * (size_t)j);
+                                if ((int)floorf(pp.x * ic) != gx || (int)floorf(pp.y * ic) != gy ||
+                                    (int)floorf(pp.z * ic) != gz)
+                                    continue;
+                                const V3 dd = ld3(pp) - hs.p;
+                                if (!(dot(dd, dd) < S.ph_r2)) continue;
+                                BRec br;
+                                br.wi = wi;
+                                br.wo = to_local(hs.sh, ld3(gld(S.ph + 3 * (size_t)j + 1)));
+                                br.measure = kMeasureSolidAngle;
+                                br.uv = hs.uv;
+                                pc = pc + bsdf_eval(B, br) * ld3(gld(S.ph + 3 * (size_t)j + 2));
+                            }
+                        }
+                return color + att * ((pc * kInvPi) / S.ph_norm);
+            }
+            const float q = smin(att.x, 0.99f);
+            if (next1D(rng) > q) return color;
+            att = att / q;
+            BRec br;
+            br.wi = to_local(hs.sh, -d);
+            br.wo = V3{0, 0, 1};
+            br.measure = kMeasureUnknown;
+            br.uv = hs.uv;
+            const V3 w = bsdf_sample(B, br, next2D(rng));
+            if (is_zero(w)) return color;  // deviation D1
+            att = att * w;
+            o = hs.p;
+            d = to_world(hs.sh, br.wo);
+            mint = kEps;
+            maxt = INF_F;
+        }
+    }
     template <int INTEG>
     ND V3 Li(Pcg &rng, V3 o, V3 d, float mint, float maxt) {
+        if constexpr (INTEG == NORI_INTEGRATOR_PHOTONMAPPER) return Li_pmap(rng, o, d, mint, maxt);
         SurfHit hs;
         if (!closest(o, d, mint, maxt, hs)) return INTEG == NORI_INTEGRATOR_AV ? V3{1, 1, 1} : V3{0, 0, 0};
         if (INTEG == NORI_INTEGRATOR_NORMALS) return V3{fabsf(hs.sh.n.x), fabsf(hs.sh.n.y), fabsf(hs.sh.n.z)};
@@ -2019,6 +2078,96 @@ __global__ __launch_bounds__(kTraceBlock) void k_direct(DevScene S, WorkDesc wd,
         atomicAdd(&C->direct_rays[0], (unsigned long long)rc);
         atomicAdd(&C->direct_rays[1], (unsigned long long)rs);
     }
+}
+
+// ------------------------------------------------------------------ photon tracing
+// PhotonMapper::preprocess (photonmapper.cpp:41-117), one thread per emitted
+// photon e (pcg32 stream wave_seed(kPhotonSeed, e), deviation D8): a light
+// chosen uniformly, AreaEmitter::samplePhoton (arealight.cpp:78-95: surface
+// point, cosine-weighted direction, power = Le * pi / pdf * lights), then
+// bounces with a stored photon at every diffuse hit, Russian roulette on the
+// red channel and BSDF sampling.  COUNT pass: photons stored per emitted
+// photon.  STORE pass (photons e < n): they go to pre[e].. in emission order,
+// and the map ends after `total` photons -- the reference's "return if the
+// map is full" (photonmapper.cpp:92-94) over the emission order.
+template <int STACK, bool STORE>
+__global__ __launch_bounds__(kTraceBlock) void k_photons(DevScene S, uint64_t e0, uint32_t n, uint32_t *count,
+                                                         const uint64_t *pre, uint64_t total, float4 *out) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
+    const uint32_t i = blockIdx.x * kTraceBlock + threadIdx.x;
+    if (i >= n) return;
+    Pcg rng;
+    wave_seed(rng, kPhotonSeed, e0 + i);
+    const uint32_t ne = S.num_emitters;
+    uint32_t li = (uint32_t)floorf((float)ne * next1D(rng));  // Scene::getRandomEmitter (scene.h:68-74)
+    if (li > ne - 1) li = ne - 1;
+    const DevEmitter &E = S.emitters[li];
+    const V2 s1 = next2D(rng), s2 = next2D(rng);
+    const DevShape &esh = S.shapes[E.shape];
+    V3 p, nrm;
+    sample_surface(S, esh, s1, p, nrm);
+    const float pdf = esh.area_norm;
+    uint64_t stored = 0;
+    const uint64_t base = STORE ? pre[i] : 0;
+    const uint64_t limit = STORE ? (total > base ? total - base : 0) : ~0ull;
+    if (pdf > 0) {  // (a light of zero area: no photon)
+        const V3 cs = to_world(frame_from(nrm), sq_cosine_hemisphere(s2));
+        const V3 ref = p + cs;  // EmitterQueryRecord(sRec.p + cosine_sample, sRec.p, sRec.n)
+        V3 power = ((emitter_eval(S, E, nrm, normalize(p - ref)) * kPi) / pdf) * (float)ne;
+        V3 o = p, d = cs;
+        uint32_t *lstk = stk + threadIdx.x;
+        for (;;) {
+            TRay r{o, d, V3{0, 0, 0}, kEps, INF_F};
+            float t, u, v;
+            uint32_t prim;
+            if (!traverse<STACK, false>(S, r, lstk, t, prim, u, v)) break;
+            const SurfHit hs = surface(S, prim, t, u, v, o, d);
+            const DevBsdf &B = S.bsdfs[S.shapes[hs.shape].bsdf];
+            if (B.type == NORI_BSDF_DIFFUSE) {
+                if (STORE) {
+                    if (stored >= limit) break;
+                    float4 *q = out + 3 * (size_t)(base + stored);
+                    q[0] = make_float4(hs.p.x, hs.p.y, hs.p.z, 0.0f);
+                    q[1] = make_float4(-d.x, -d.y, -d.z, 0.0f);
+                    q[2] = make_float4(power.x, power.y, power.z, 0.0f);
+                }
+                ++stored;
+            }
+            const float q = smin(power.x, 0.99f);
+            if (next1D(rng) > q) break;
+            power = power / q;
+            BRec br;
+            br.wi = to_local(hs.sh, -d);
+            br.wo = V3{0, 0, 1};
+            br.measure = kMeasureUnknown;
+            br.uv = hs.uv;
+            const V3 w = bsdf_sample(B, br, next2D(rng));
+            if (is_zero(w)) break;  // deviation D1
+            power = power * w;
+            o = hs.p;
+            d = to_world(hs.sh, br.wo);
+        }
+    }
+    if (!STORE) count[i] = (uint32_t)(stored < 0xFFFFFFFFull ? stored : 0xFFFFFFFFull);
+}
+
+template <bool STORE>
+static void photons_dispatch(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *count, const uint64_t *pre,
+                             uint64_t total, float4 *out, int stack, hipStream_t st) {
+    const dim3 g((n + kTraceBlock - 1) / kTraceBlock), b(kTraceBlock);
+    switch (stack) {
+    case 0: hipLaunchKernelGGL((k_photons<0, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
+    case 8: hipLaunchKernelGGL((k_photons<8, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
+    case 16: hipLaunchKernelGGL((k_photons<16, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
+    default: hipLaunchKernelGGL((k_photons<32, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
+    }
+}
+hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *count, const uint64_t *pre,
+                          uint64_t total, float4 *out, int stack, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (out) photons_dispatch<true>(S, e0, n, count, pre, total, out, stack, st);
+    else photons_dispatch<false>(S, e0, n, count, pre, total, out, stack, st);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ film splat
@@ -2324,6 +2473,7 @@ hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Cou
     case NORI_INTEGRATOR_DIRECT_EMS: direct_dispatch<NORI_INTEGRATOR_DIRECT_EMS>(S, wd, rec, C, stack, st); break;
     case NORI_INTEGRATOR_DIRECT_MATS: direct_dispatch<NORI_INTEGRATOR_DIRECT_MATS>(S, wd, rec, C, stack, st); break;
     case NORI_INTEGRATOR_DIRECT_MIS: direct_dispatch<NORI_INTEGRATOR_DIRECT_MIS>(S, wd, rec, C, stack, st); break;
+    case NORI_INTEGRATOR_PHOTONMAPPER: direct_dispatch<NORI_INTEGRATOR_PHOTONMAPPER>(S, wd, rec, C, stack, st); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -201,6 +201,7 @@ struct nori_gpu_ctx {
     DevBuf q[2][6], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
     DevBuf ptctr;                    // persistent traversal work counters, 4 per part
     DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
+    DevBuf ph, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
     uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
@@ -391,10 +392,17 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         emitters[i].cos_tw = e.cos_total_width;
         if (e.type == NORI_EMITTER_ENVMAP) build_envmap(e, emitters[i], env);
     }
-    if (d.integrator < NORI_INTEGRATOR_PATH_MATS || d.integrator > NORI_INTEGRATOR_DIRECT_MIS)
+    if (d.integrator < NORI_INTEGRATOR_PATH_MATS || d.integrator > NORI_INTEGRATOR_PHOTONMAPPER)
         throw NoriException(NORI_ERR_UNSUPPORTED, "unknown integrator");
     if (d.num_emitters == 0 && d.integrator != NORI_INTEGRATOR_NORMALS && d.integrator != NORI_INTEGRATOR_AV)
         throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
+    if (d.integrator == NORI_INTEGRATOR_PHOTONMAPPER) {
+        if (d.photon_count == 0 || !(d.photon_radius > 0.0f) || !std::isfinite(d.photon_radius))
+            throw NoriException(NORI_ERR_INVALID, "photonmapper: photon_count and photon_radius must be positive");
+        for (uint32_t i = 0; i < d.num_emitters; ++i)  // Emitter::samplePhoton (emitter.h) throws for the others
+            if (d.emitters[i].type != NORI_EMITTER_AREA)
+                throw NoriException(NORI_ERR_UNSUPPORTED, "photonmapper: photons from area lights only");
+    }
     if (d.camera.camera_type < NORI_CAMERA_PERSPECTIVE || d.camera.camera_type > NORI_CAMERA_ADVANCED)
         throw NoriException(NORI_ERR_UNSUPPORTED, "unknown camera type");
     // the reference leaves Scene::m_medium uninitialised without a <medium>
@@ -698,6 +706,53 @@ void var_finish(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, bool cancelled)
     std::vector<float> h(n);
     HIP_TRY(hipMemcpy(h.data(), c.varbuf.p, n * sizeof(float), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < n; ++i) rd.variance_out[i] += h[i];
+}
+
+// PhotonMapper::preprocess (photonmapper.cpp:41-117): photons are traced on
+// the device in emission order batches (k_photons count pass) until the
+// stored count reaches photonCount, then the emitted photons that contribute
+// are traced again writing their photons (store pass), and the host stores
+// them as the reference's PhotonData and builds the hash grid.
+void photon_preprocess(nori_gpu_ctx &c, const nori_scene_desc &d) {
+    const uint64_t N = d.photon_count;
+    const uint32_t batch = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(N, 1u << 20), 1u << 24);
+    DevBuf cnt;
+    cnt.ensure(4 * (size_t)batch);
+    std::vector<uint32_t> hc(batch);
+    std::vector<uint64_t> pre;  // photons stored before each emitted photon
+    uint64_t total = 0, e0 = 0;
+    while (total < N) {
+        if (e0 >= 64 * N + batch)  // the reference would loop forever
+            throw NoriException(NORI_ERR_INVALID, "photonmapper: photons do not reach a diffuse surface");
+        HIP_TRY(launch_photons(c.S, e0, batch, cnt.as<uint32_t>(), nullptr, 0, nullptr, c.stack, c.stream));
+        HIP_TRY(hipMemcpyAsync(hc.data(), cnt.p, 4 * (size_t)batch, hipMemcpyDeviceToHost, c.stream));
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        for (uint32_t i = 0; i < batch && total < N; ++i) {
+            pre.push_back(total);
+            total += hc[i];
+        }
+        e0 += batch;
+    }
+    DevBuf dpre, out;
+    dpre.upload(pre);
+    out.ensure(48 * (size_t)N);
+    HIP_TRY(launch_photons(c.S, 0, (uint32_t)pre.size(), nullptr, dpre.as<uint64_t>(), N, out.as<float4>(), c.stack,
+                           c.stream));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    std::vector<float> raw(12 * (size_t)N), ph;
+    HIP_TRY(hipMemcpy(raw.data(), out.p, 48 * (size_t)N, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> start;
+    uint32_t mask = 0;
+    build_photon_map(raw, (uint32_t)N, d.photon_radius, ph, start, mask);
+    c.ph.upload(ph);
+    c.ph_start.upload(start);
+    const float r = d.photon_radius;
+    c.S.ph = c.ph.as<float4>();
+    c.S.ph_start = c.ph_start.as<uint32_t>();
+    c.S.ph_mask = mask;
+    c.S.ph_inv_cell = 1.0f / r;
+    c.S.ph_r2 = r * r;                                 // kdtree.h:266
+    c.S.ph_norm = (r * r) * (float)d.photon_count;     // photonmapper.cpp:177
 }
 
 // normals / av / direct*: no path pool -- per chunk of passes, k_direct runs
@@ -1188,6 +1243,7 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         upload_scene(*c, *d);
         setup_persistent(*c);
+        if (d->integrator == NORI_INTEGRATOR_PHOTONMAPPER) photon_preprocess(*c, *d);
         *out = c.release();
         return NORI_OK;
     });

@@ -362,7 +362,7 @@ struct Registrar {
 struct Unsupported : NoriObject {
     EClassType getClassType() const override { return EClassTypeCount; }
 };
-static const char *kUnsupported[] = {"photonmapper", "checkerboard_float", "image_texture", "normal_map", "perlin",
+static const char *kUnsupported[] = {"checkerboard_float", "image_texture", "normal_map", "perlin",
                                      "chi2test"};
 
 // ---- textures (consttexture.cpp)
@@ -808,6 +808,14 @@ struct DirectMats : Integrator { explicit DirectMats(const PropertyList &) : Int
 NORI_REGISTER_CLASS(DirectMats, "direct_mats")
 struct DirectMis : Integrator { explicit DirectMis(const PropertyList &) : Integrator(NORI_INTEGRATOR_DIRECT_MIS) {} };
 NORI_REGISTER_CLASS(DirectMis, "direct_mis")
+struct PhotonMapper : Integrator {  // photonmapper.cpp:34-39
+    int count;
+    float radius;
+    explicit PhotonMapper(const PropertyList &p)
+        : Integrator(NORI_INTEGRATOR_PHOTONMAPPER), count(p.getInteger("photonCount", 1000000)),
+          radius(p.getFloat("photonRadius", 0.0f)) {}
+};
+NORI_REGISTER_CLASS(PhotonMapper, "photonmapper")
 struct Phase : NoriObject {
     explicit Phase(const PropertyList &) {}
     EClassType getClassType() const override { return EPhaseFunction; }
@@ -1119,6 +1127,21 @@ HostScene *load_scene_xml(const std::string &path, int width, int height, int sp
     if (hs->emitters.empty() && integ != NORI_INTEGRATOR_NORMALS && integ != NORI_INTEGRATOR_AV)
         throw NoriException(NORI_ERR_INVALID, "the scene has no emitter");
     if (integ == NORI_INTEGRATOR_AV) hs->desc.av_length = static_cast<AverageVisibility *>(sc->integrator)->length;
+    if (integ == NORI_INTEGRATOR_PHOTONMAPPER) {
+        auto *pm = static_cast<PhotonMapper *>(sc->integrator);
+        if (pm->count <= 0) throw NoriException(NORI_ERR_INVALID, "photonmapper: photonCount must be positive");
+        for (const nori_emitter_desc &e : hs->emitters)  // Emitter::samplePhoton (emitter.h:106-108)
+            if (e.type != NORI_EMITTER_AREA)
+                throw NoriException(NORI_ERR_UNSUPPORTED, "Emitter::samplePhoton(): not implemented!");
+        float r = pm->radius;
+        if (r == 0) {  // photonmapper.cpp:55-56: scene bounding box diagonal / 500
+            const float e0 = hs->root_max[0] - hs->root_min[0], e1 = hs->root_max[1] - hs->root_min[1],
+                        e2 = hs->root_max[2] - hs->root_min[2];
+            r = std::sqrt((e0 * e0 + e1 * e1) + e2 * e2) / 500.0f;
+        }
+        hs->desc.photon_count = (uint32_t)pm->count;
+        hs->desc.photon_radius = r;
+    }
     nori_camera_desc cam = sc->camera->d;
     if (width > 0) cam.width = width;
     if (height > 0) cam.height = height;

@@ -1,4 +1,4 @@
-"""ctypes mirror of include/nori_gpu.h (ABI version 3).
+"""ctypes mirror of include/nori_gpu.h (ABI version 4).
 
 The structures below must match the C declarations field for field; the
 test suite checks their sizes against the library (tests/test_abi.py).
@@ -6,7 +6,7 @@ test suite checks their sizes against the library (tests/test_abi.py).
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 NORI_OK = 0
 NORI_ERR_INVALID = -1
@@ -23,9 +23,10 @@ EMITTER_AREA, EMITTER_ENVMAP, EMITTER_POINT, EMITTER_SPOT = 0, 1, 2, 3
 TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD = 0, 1
 CAMERA_PERSPECTIVE, CAMERA_THINLENS, CAMERA_ADVANCED = 0, 1, 2
 (INTEGRATOR_PATH_MATS, INTEGRATOR_PATH_MIS, INTEGRATOR_VOLUMETRIC, INTEGRATOR_NORMALS, INTEGRATOR_AV,
- INTEGRATOR_DIRECT, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS) = range(9)
+ INTEGRATOR_DIRECT, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS,
+ INTEGRATOR_PHOTONMAPPER) = range(10)
 INTEGRATOR_NAMES = {0: "path_mats", 1: "path_mis", 2: "volumetric", 3: "normals", 4: "av", 5: "direct",
-                    6: "direct_ems", 7: "direct_mats", 8: "direct_mis"}
+                    6: "direct_ems", 7: "direct_mats", 8: "direct_mis", 9: "photonmapper"}
 RNG_WAVE, RNG_BLOCK = 0, 1
 BLOCK_SIZE = 32
 FILTER_RESOLUTION = 32
@@ -79,7 +80,7 @@ class SceneDesc(C.Structure):
                 ("bsdfs", C.POINTER(BsdfDesc)), ("num_emitters", C.c_uint32),
                 ("emitters", C.POINTER(EmitterDesc)), ("camera", CameraDesc),
                 ("medium", MediumDesc), ("integrator", C.c_int32), ("sample_count", C.c_uint32),
-                ("av_length", C.c_float)]
+                ("av_length", C.c_float), ("photon_count", C.c_uint32), ("photon_radius", C.c_float)]
 
 
 class RenderDesc(C.Structure):

@@ -558,6 +558,8 @@ struct oracle_scene {
     float av_length;
     /* thinlens / advancedCamera */
     int cam_type; float lens_radius, focal; float distortion[2]; V3 chromatic;
+    /* photonmapper: photons (position, direction, power) after PhotonData */
+    float *ph; uint32_t nph; float ph_r, ph_norm; uint64_t ph_emitted;
 };
 
 static inline V3 vtx(const oracle_scene *s, uint32_t i) { return v3(s->P[3 * i], s->P[3 * i + 1], s->P[3 * i + 2]); }
@@ -1369,6 +1371,128 @@ static V3 Li_direct_mats_mis(const oracle_scene *s, Pcg *rng, const Ray *ray, Co
     return vadd(color, vmul(vmuls(w, w_mat), Le));
 }
 
+/* ---- photon mapper (photonmapper.cpp, photon.h / photon.cpp) ------------- */
+/* PhotonData lookup tables (photon.cpp:30-41) */
+static float ph_cos_phi[256], ph_sin_phi[256], ph_cos_theta[256], ph_sin_theta[256], ph_exp[256];
+static pthread_once_t ph_once = PTHREAD_ONCE_INIT;
+static void ph_tables(void) {
+    for (int i = 0; i < 256; i++) {
+        float angle = (float)i * (F_PI / 256.0f);
+        ph_cos_phi[i] = cosf(2.0f * angle); ph_sin_phi[i] = sinf(2.0f * angle);
+        ph_cos_theta[i] = cosf(angle); ph_sin_theta[i] = sinf(angle);
+        ph_exp[i] = ldexpf(1.0f, i - (128 + 8));
+    }
+    ph_exp[0] = 0;
+}
+/* PhotonData(dir, power) (photon.cpp:43-74) followed by getDirection /
+ * getPower (photon.h:44-55): the values the density estimate sees */
+static void photon_store(float *dst, V3 p, V3 dir, V3 power) {
+    int th = (int)(acosf(dir.z) * (256.0f / F_PI));                /* float: common.h:56 */
+    uint8_t theta = (uint8_t)(th < 255 ? th : 255);
+    int tmp = (int)(atan2f(dir.y, dir.x) * (256.0f / (2.0f * F_PI)));
+    if (tmp > 255) tmp = 255;
+    uint8_t phi = (uint8_t)(tmp < 0 ? tmp + 256 : tmp);
+    uint8_t rgbe[4] = {0, 0, 0, 0};
+    float mx = vmaxc(power);
+    if (!(mx < 1e-32)) {
+        int e;
+        mx = frexpf(mx, &e) * 256.0f / mx;
+        rgbe[0] = (uint8_t)(power.x * mx); rgbe[1] = (uint8_t)(power.y * mx); rgbe[2] = (uint8_t)(power.z * mx);
+        rgbe[3] = (uint8_t)(e + 128);
+    }
+    dst[0] = p.x; dst[1] = p.y; dst[2] = p.z;
+    dst[3] = ph_cos_phi[phi] * ph_sin_theta[theta];
+    dst[4] = ph_sin_phi[phi] * ph_sin_theta[theta];
+    dst[5] = ph_cos_theta[theta];
+    float sc = ph_exp[rgbe[3]];
+    dst[6] = (float)rgbe[0] * sc; dst[7] = (float)rgbe[1] * sc; dst[8] = (float)rgbe[2] * sc;
+}
+/* PhotonMapper::preprocess (photonmapper.cpp:41-117), sequential over the
+ * emitted photons; photon e draws from its own stream wave_seed(kPhotonSeed,
+ * e) (deviation D8: the reference draws every photon from one independent
+ * sampler).  Stops at the photonCount-th stored photon, as the reference. */
+#define ORACLE_PHOTON_SEED 0x70686f746f6e6d70ull
+static int photon_preprocess(oracle_scene *s) {
+    pthread_once(&ph_once, ph_tables);
+    const uint64_t N = s->desc.photon_count;
+    s->ph = (float *)malloc(sizeof(float) * 9 * (N ? N : 1));
+    if (!s->ph) return -1;
+    s->nph = 0;
+    const uint32_t ne = s->nemitters;
+    for (uint64_t e = 0; s->nph < N; ++e) {
+        if (e >= 64 * N + (1u << 20)) return -1;  /* nothing reaches a diffuse surface */
+        Pcg rng;
+        wave_seed(&rng, ORACLE_PHOTON_SEED, e);
+        const Emitter *light = random_emitter(s, next1D(&rng));
+        V2 s1 = next2D(&rng), s2 = next2D(&rng);
+        V3 p, n; float pdf;
+        shape_sample_surface(s, &s->shapes[light->shape], s1, &p, &n, &pdf);
+        if (pdf <= 0) continue;                                     /* arealight.cpp:84-85 */
+        Frame f = frame_from(n);
+        V3 cs = to_world(&f, sq_cosine_hemisphere(s2));
+        ERec er = erec_hit(vadd(p, cs), p, n);                      /* arealight.cpp:92-94 */
+        V3 power = vmuls(vdivs(vmuls(emitter_eval(light, &er), F_PI), pdf), (float)ne);
+        Ray ray = ray_make(p, cs, EPS, F_INF);
+        for (;;) {
+            Its its;
+            if (!scene_intersect(s, &ray, &its, 0)) break;
+            const Bsdf *b = &s->bsdfs[s->shapes[its.shape].bsdf];
+            if (b->type == NORI_BSDF_DIFFUSE) {
+                photon_store(&s->ph[9 * s->nph], its.p, vneg(ray.d), power);
+                if (++s->nph == N) { s->ph_emitted = e + 1; return 0; }
+            }
+            float q = smin(power.x, 0.99f);
+            if (next1D(&rng) > q) break;
+            power = vdivs(power, q);
+            BRec br; memset(&br, 0, sizeof(br));
+            br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv;
+            V3 w = bsdf_sample(b, &br, next2D(&rng));
+            if (vzero(w)) break;                                    /* D1 */
+            power = vmul(power, w);
+            ray = ray_make(its.p, to_world(&its.sh, br.wo), EPS, F_INF);
+        }
+    }
+    return 0;
+}
+/* PhotonMapper::Li (photonmapper.cpp:119-196); the kd-tree radius search is
+ * a scan over every photon with |x - p|^2 < r^2 (kdtree.h:260-316). */
+static V3 Li_pmap(const oracle_scene *s, Pcg *rng, const Ray *ray0, Counters *c) {
+    V3 color = v3(0, 0, 0), att = v3(1, 1, 1);
+    Ray ray = *ray0;
+    const float r2 = s->ph_r * s->ph_r;
+    for (;;) {
+        Its its;
+        c->closest++;
+        if (!scene_intersect(s, &ray, &its, 0)) return color;
+        color = vadd(color, vmul(att, hit_emission(s, &its, ray.o)));
+        const Bsdf *b = &s->bsdfs[s->shapes[its.shape].bsdf];
+        if (b->type == NORI_BSDF_DIFFUSE) {
+            V3 pc = v3(0, 0, 0);
+            V3 wi = to_local(&its.sh, vneg(ray.d));
+            for (uint32_t j = 0; j < s->nph; ++j) {
+                const float *q = &s->ph[9 * (size_t)j];
+                V3 dd = vsub(v3(q[0], q[1], q[2]), its.p);
+                if (!(vdot(dd, dd) < r2)) continue;
+                BRec br; memset(&br, 0, sizeof(br));
+                br.wi = wi; br.wo = to_local(&its.sh, v3(q[3], q[4], q[5]));
+                br.measure = M_SOLID_ANGLE; br.eta = 1.0f; br.uv = its.uv;
+                pc = vadd(pc, vmul(bsdf_eval(b, &br), v3(q[6], q[7], q[8])));
+            }
+            return vadd(color, vmul(att, vdivs(vmuls(pc, F_INV_PI), s->ph_norm)));
+        }
+        float q = smin(att.x, 0.99f);
+        if (next1D(rng) > q) return color;
+        att = vdivs(att, q);
+        BRec br; memset(&br, 0, sizeof(br));
+        br.wi = to_local(&its.sh, vneg(ray.d)); br.uv = its.uv;
+        V3 w = bsdf_sample(b, &br, next2D(rng));
+        if (vzero(w)) return color;                                 /* D1 */
+        att = vmul(att, w);
+        c->bounces++;
+        ray = ray_make(its.p, to_world(&its.sh, br.wo), EPS, F_INF);
+    }
+}
+
 static inline V3 Li(const oracle_scene *s, Pcg *rng, const Ray *ray, Counters *c) {
     switch (s->integrator) {
     case NORI_INTEGRATOR_PATH_MATS: return Li_mats(s, rng, ray, c);
@@ -1379,6 +1503,7 @@ static inline V3 Li(const oracle_scene *s, Pcg *rng, const Ray *ray, Counters *c
     case NORI_INTEGRATOR_DIRECT_EMS: return Li_direct_lights(s, rng, ray, c, 1);
     case NORI_INTEGRATOR_DIRECT_MATS: return Li_direct_mats_mis(s, rng, ray, c, 0);
     case NORI_INTEGRATOR_DIRECT_MIS: return Li_direct_mats_mis(s, rng, ray, c, 1);
+    case NORI_INTEGRATOR_PHOTONMAPPER: return Li_pmap(s, rng, ray, c);
     default: return Li_mis(s, rng, ray, c);
     }
 }
@@ -1673,6 +1798,15 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
         oracle_scene_free(s); return NORI_ERR_INVALID;
     }
     if (bvh_build(s) != 0) { oracle_scene_free(s); return NORI_ERR_OOM; }
+    if (s->integrator == NORI_INTEGRATOR_PHOTONMAPPER) {
+        for (uint32_t i = 0; i < s->nemitters; ++i)
+            if (s->emitters[i].type != NORI_EMITTER_AREA) { oracle_scene_free(s); return NORI_ERR_UNSUPPORTED; }
+        s->ph_r = d->photon_radius;
+        s->ph_norm = (s->ph_r * s->ph_r) * (float)d->photon_count;   /* photonmapper.cpp:177 */
+        if (!(s->ph_r > 0) || d->photon_count == 0 || photon_preprocess(s) != 0) {
+            oracle_scene_free(s); return NORI_ERR_INVALID;
+        }
+    }
     *out = s;
     return NORI_OK;
 }
@@ -1684,8 +1818,13 @@ void oracle_scene_free(oracle_scene *s) {
         free(s->emitters[i].pdf); free(s->emitters[i].cdf); free(s->emitters[i].pmarg); free(s->emitters[i].cmarg);
     }
     free(s->shapes); free(s->shape_offset); free(s->bsdfs); free(s->emitters);
-    free(s->nodes); free(s->indices);
+    free(s->nodes); free(s->indices); free(s->ph);
     free(s);
+}
+int oracle_photon_map(const oracle_scene *s, uint64_t *emitted, uint32_t *count, const float **photons) {
+    if (!s || !s->ph) return NORI_ERR_INVALID;
+    *emitted = s->ph_emitted; *count = s->nph; *photons = s->ph;
+    return NORI_OK;
 }
 uint32_t oracle_scene_node_count(const oracle_scene *s) { return s ? s->nnodes : 0; }
 /* BVH::statistics (bvh.cpp:384-402) over the tree reachable from the root */

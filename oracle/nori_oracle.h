@@ -58,6 +58,10 @@ int oracle_trace(const oracle_scene *s, const float *rays, uint32_t n, int any_h
 int oracle_wave_samples(const oracle_scene *s, uint64_t seed, const uint64_t *sample_ids,
                         uint32_t n, float *out);
 
+/* photonmapper scenes: photons emitted to fill the map and the map itself
+ * (n x 9 floats: position, direction, power as PhotonData returns them). */
+int oracle_photon_map(const oracle_scene *s, uint64_t *emitted, uint32_t *count, const float **photons);
+
 /* pcg32 (ext/pcg32/pcg32.h:51-110). state2 = {state, inc}. */
 void oracle_pcg32_seed(uint64_t *state2, uint64_t initstate, uint64_t initseq);
 uint32_t oracle_pcg32_next(uint64_t *state2);

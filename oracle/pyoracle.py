@@ -56,6 +56,7 @@ def lib():
             "oracle_bsdf_ttest": (C.c_int, [vp, f32, u32, pd, pd]),
             "oracle_bsdf_sample": (C.c_int, [vp, pf, pf, u32, pf]),
             "oracle_bsdf_eval_pdf": (C.c_int, [vp, pf, pf, u32, pf]),
+            "oracle_photon_map": (C.c_int, [vp, C.POINTER(u64), C.POINTER(u32), C.POINTER(pf)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(l, name)
@@ -153,6 +154,14 @@ class OracleScene:
 
     def node_count(self):
         return lib().oracle_scene_node_count(self._h)
+
+    def photon_map(self):
+        """(emitted photons, photons n x 9: position, direction, power after PhotonData)."""
+        e, n, p = C.c_uint64(), C.c_uint32(), C.POINTER(C.c_float)()
+        rc = lib().oracle_photon_map(self._h, C.byref(e), C.byref(n), C.byref(p))
+        if rc != 0:
+            raise RuntimeError(f"oracle_photon_map: {rc}")
+        return e.value, np.ctypeslib.as_array(p, shape=(n.value, 9)).copy()
 
     def bvh_stats(self):
         """(reachable nodes, BVH::statistics SAH cost, FNV-1a hash of the leaf-order primitive ids)."""
