@@ -9,6 +9,7 @@
  *                            + NoriObjectFactory::createInstance  include/nori/object.h:160-165
  *                            + Scene::activate()          src/scene.cpp:43-61
  *   nori_gpu_create       <- Scene::activate's BVH::build src/bvh.cpp:329-382 (flatten + upload)
+ *                            and Integrator::preprocess    src/photonmapper.cpp:41-117 (photon map)
  *   nori_gpu_render       <- RenderThread::renderScene's pass loop
  *                            src/render.cpp:173-250 (tbb::parallel_for over blocks,
  *                            renderBlock render.cpp:80-133, Integrator::Li
@@ -21,6 +22,8 @@
  *   nori_film_develop     <- ImageBlock::toBitmap         src/block.cpp:76-82
  *   nori_write_exr        <- Bitmap::save                 src/bitmap.cpp:82-107
  *   nori_read_exr         <- Bitmap::Bitmap(filename)     src/bitmap.cpp:23-80
+ *   nori_write_png        <- Bitmap::saveToLDR            src/bitmap.cpp:122-148
+ *   nori_film_variance    <- renderScene's variance image src/render.cpp:164-169,190-245
  *   nori_scene_bvh_info   <- BVH::build/statistics        src/bvh.cpp:329-402
  *
  * Rules of the ABI: plain C types only, no exceptions cross it, every call
