@@ -22,8 +22,9 @@
  *   nori_film_develop     <- ImageBlock::toBitmap         src/block.cpp:76-82
  *   nori_write_exr        <- Bitmap::save                 src/bitmap.cpp:82-107
  *   nori_read_exr         <- Bitmap::Bitmap(filename)     src/bitmap.cpp:23-80
- *   nori_write_png        <- Bitmap::saveToLDR            src/bitmap.cpp:122-148
+ *   nori_write_png        <- Bitmap::saveToLDR            src/bitmap.cpp:122-139
  *   nori_film_variance    <- renderScene's variance image src/render.cpp:164-169,190-245
+ *   nori_denoise          <- denoiser/denoiser.py:53-66 (NL-means)
  *   nori_scene_bvh_info   <- BVH::build/statistics        src/bvh.cpp:329-402
  *
  * Rules of the ABI: plain C types only, no exceptions cross it, every call
@@ -225,6 +226,17 @@ int nori_write_png(const char *path, const float *rgb, int width, int height);
  * 263-276: the spread of the running mean over the passes) does not estimate
  * the pixel variance; this one does (deviation D5). */
 int nori_film_variance(const nori_scene_desc *scene, const float *stats, float *out);
+
+/* NL-means denoiser <- denoiser/denoiser.py:53-66 on the GPU.  rgb: H x W x 3
+ * image, variance: H x W per-pixel variance (the script's grey variance
+ * image), out: H x W x 3.  radius = r (offsets in [-r, r]^2, <= 8), patch = f
+ * (box filters of width 2(f-1)+1, 1 <= f <= 5), k = the script's k (0.02).
+ * mode 0 reproduces the script's d2 (both variance terms 2 var(neighbour)),
+ * mode 1 the textbook form (var_p + min(var_p, var_q), var_p + var_q).
+ * Neighbours wrap around the image (np.roll), the box filters zero-pad
+ * (convolve2d mode 'same').  Host buffers; runs on `device`. */
+int nori_denoise(int device, const float *rgb, const float *variance, int width, int height, int radius,
+                 int patch, float k, int mode, float *out);
 /* Read the R, G, B planes of a scanline OpenEXR file (NONE/ZIPS/ZIP, HALF or
  * FLOAT) <- Bitmap::Bitmap (bitmap.cpp:23-80).  Call with rgb = NULL to get
  * the size, then with a buffer of 3*width*height floats (row-major). */

@@ -76,6 +76,11 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 // photon mapper: one thread per work id of wd (pass-major, pixels in
 // wd.pixels order) writes its record.
 hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack, hipStream_t st);
+// NL-means denoiser (denoise.hip, denoiser/denoiser.py): img W x H x 3,
+// var W x H, radius R (offsets), box half-width P (= the script's f - 1).
+size_t denoise_lds_bytes(int R, int P);
+hipError_t launch_denoise(const float *img, const float *var, int W, int H, int R, int P, float k, int mode,
+                          float *out, hipStream_t st);
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 

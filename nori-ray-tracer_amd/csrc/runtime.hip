@@ -1156,6 +1156,30 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
 extern "C" {
 
 const char *nori_gpu_last_error(void) { return g_last_error.c_str(); }
+
+// denoiser/denoiser.py (NL-means over a rendered image and its per-pixel
+// variance) on device `device`: host buffers in, host buffer out.
+int nori_denoise(int device, const float *rgb, const float *variance, int width, int height, int radius, int patch,
+                 float k, int mode, float *out) {
+    return guarded([&] {
+        if (!rgb || !variance || !out || width <= 0 || height <= 0 || radius < 0 || radius > 8 || patch < 1 ||
+            patch > 5 || mode < 0 || mode > 1 || !(k > 0.0f))
+            return fail(NORI_ERR_INVALID, "nori_denoise: invalid arguments");
+        HIP_TRY(hipSetDevice(device));
+        const size_t n = (size_t)width * (size_t)height;
+        DevBuf di, dv, dout;
+        di.ensure(12 * n);
+        dv.ensure(4 * n);
+        dout.ensure(12 * n);
+        HIP_TRY(hipMemcpy(di.p, rgb, 12 * n, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(dv.p, variance, 4 * n, hipMemcpyHostToDevice));
+        HIP_TRY(launch_denoise((const float *)di.p, (const float *)dv.p, width, height, radius, patch - 1, k, mode,
+                               (float *)dout.p, nullptr));
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(out, dout.p, 12 * n, hipMemcpyDeviceToHost));
+        return (int)NORI_OK;
+    });
+}
 int nori_gpu_abi_version(void) { return NORI_GPU_ABI_VERSION; }
 
 int nori_scene_load_xml(const char *path, int width, int height, int spp, nori_scene **out) {

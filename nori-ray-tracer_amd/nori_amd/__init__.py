@@ -25,7 +25,8 @@ from . import _abi
 from ._abi import NoriError, check, lib  # noqa: F401
 
 __all__ = ["load_scene", "Scene", "GpuRenderer", "RenderThread", "NoriError", "device_count",
-           "develop", "write_exr", "write_png", "read_exr", "film_variance"]
+           "develop", "write_exr", "write_png", "read_exr", "film_variance", "ldr_bytes", "variance_gray",
+           "denoise"]
 
 
 def _fptr(a):
@@ -142,6 +143,49 @@ def film_variance(scene, stats):
     out = np.zeros((scene.height, scene.width, 3), np.float32)
     check(lib().nori_film_variance(scene.desc_ptr, _fptr(stats), _fptr(out)))
     return out
+
+
+def ldr_bytes(rgb):
+    """The 8-bit sRGB values Bitmap::saveToLDR writes (bitmap.cpp:122-139;
+    nori_write_png): (uint8) clamp(255 * GammaCorrect(v) + 0.5, 0, 255), float32."""
+    v = np.asarray(rgb, np.float32)
+    with np.errstate(invalid="ignore"):
+        g = np.where(v <= np.float32(0.0031308), np.float32(12.92) * v,
+                     np.float32(1.055) * np.power(np.maximum(v, 0).astype(np.float32), np.float32(1.0 / 2.4))
+                     - np.float32(0.055)).astype(np.float32)
+    return np.clip(np.float32(255) * g + np.float32(0.5), 0, 255).astype(np.uint8)
+
+
+def variance_gray(var_rgb):
+    """The variance image denoiser.py:19-21 reads: the `<stem>_variance.exr`
+    taken to an 8-bit PNG by hdrToLdr (saveToLDR), loaded by OpenCV as BGR
+    and converted with COLOR_RGB2GRAY -- so the blue byte takes the red
+    weight -- then divided by 255.  OpenCV's 8-bit grey conversion is fixed
+    point: (4899 c0 + 9617 c1 + 1868 c2 + 2^13) >> 14.  (OpenCV is not in
+    this image: this step is a restatement, unpinned.)"""
+    b = ldr_bytes(var_rgb).astype(np.int64)
+    bgr = b[..., ::-1]
+    gray = (4899 * bgr[..., 0] + 9617 * bgr[..., 1] + 1868 * bgr[..., 2] + (1 << 13)) >> 14
+    return (gray.astype(np.float64) / 255.0).astype(np.float32)
+
+
+def denoise(img, var, radius=3, patch=3, k=0.02, mode=0, device=0, script_scale=True):
+    """NL-means denoiser (denoiser/denoiser.py) on the GPU (nori_denoise).
+
+    img: (H, W, 3) linear image; var: (H, W) per-pixel variance in the
+    script's units (variance_gray()).  script_scale: divide the image by 255
+    first, as the script does with its EXR input (denoiser.py:16), and return
+    the result in the input's scale.  mode 0 = the script's distance (both
+    variance terms 2 var(neighbour)), 1 = the textbook form."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    var = np.ascontiguousarray(var, dtype=np.float32)
+    if img.ndim != 3 or img.shape[2] != 3 or var.shape != img.shape[:2]:
+        raise ValueError(f"image {img.shape} / variance {var.shape}: expected (H, W, 3) and (H, W)")
+    src = np.ascontiguousarray(img / np.float32(255)) if script_scale else img
+    out = np.empty_like(src)
+    check(lib().nori_denoise(device, _fptr(src), _fptr(var), img.shape[1], img.shape[0], radius, patch, k, mode,
+                             _fptr(out)))
+    return out * np.float32(255) if script_scale else out
 
 
 class BvhInfo(C.Structure):

@@ -120,6 +120,8 @@ SIGNATURES = {
     "nori_write_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, C.c_int]),
     "nori_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, C.c_int]),
     "nori_film_variance": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "nori_denoise": (C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int,
+                               C.c_int, C.c_float, C.c_int, C.POINTER(C.c_float)]),
     "nori_read_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)]),
     "nori_scene_bvh_info": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nori_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
