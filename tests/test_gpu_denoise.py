@@ -45,16 +45,20 @@ def test_denoise_parameters(built, radius, patch):
 
 
 def test_denoise_rendered_cbox(built, tmp_path):
-    """A 16-spp path_mis render with its variance image, denoised as the
-    script would (EXR / 255, grey 8-bit variance): parity with the checker
-    and a lower error against a 512-spp render than the noisy input."""
+    """A 16-spp path_mis render with its variance image.  (1) Denoised as the
+    script would (EXR / 255, grey 8-bit variance): parity with the checker.
+    With the script's distance and scales every weight saturates at 1, so
+    its output is a plain box blur -- the MSE against a 512-spp render is
+    printed, not asserted.  (2) The textbook distance on linear values with
+    the summed per-channel variance of each pixel mean lowers the MSE."""
     from conftest import scene_path
 
     s = nori_amd.load_scene(scene_path("pa4/cbox/cbox_path_mis.xml"), 160, 120, 16)
     stats = np.zeros((s.height, s.width, 8), np.float32)
     with nori_amd.GpuRenderer(s, 0) as r:
         noisy = nori_amd.develop(s, r.render(variance=stats))
-    var = nori_amd.variance_gray(nori_amd.film_variance(s, stats))
+    fvar = nori_amd.film_variance(s, stats)
+    var = nori_amd.variance_gray(fvar)
     ref_s = nori_amd.load_scene(scene_path("pa4/cbox/cbox_path_mis.xml"), 160, 120, 512)
     with nori_amd.GpuRenderer(ref_s, 0) as r:
         clean = nori_amd.develop(ref_s, r.render())
@@ -63,12 +67,15 @@ def test_denoise_rendered_cbox(built, tmp_path):
     t1 = time.perf_counter()
     chk = nlmeans_check.nlmeans(noisy / 255.0, var) * 255.0
     err = float((np.abs(den - chk) / np.maximum(np.abs(chk), 1e-2)).max())
-    mse_noisy = float(np.mean((np.clip(noisy, 0, 1) - np.clip(clean, 0, 1)) ** 2))
-    mse_den = float(np.mean((np.clip(den, 0, 1) - np.clip(clean, 0, 1)) ** 2))
+
+    def mse(a):
+        return float(np.mean((np.clip(a, 0, 1) - np.clip(clean, 0, 1)) ** 2))
+
+    tb = nori_amd.denoise(noisy, fvar.sum(axis=2), mode=1, script_scale=False)
     print(f"cbox 160x120: denoise {1e3 * (t1 - t0):.2f} ms (host buffers), max rel err {err:.2e}, "
-          f"MSE vs 512 spp: noisy {mse_noisy:.3e} -> denoised {mse_den:.3e}")
+          f"MSE vs 512 spp: noisy {mse(noisy):.3e}, script {mse(den):.3e}, textbook linear {mse(tb):.3e}")
     assert err < 2e-4
-    assert mse_den < mse_noisy
+    assert mse(tb) < mse(noisy)
 
 
 def test_denoise_cli(built, tmp_path):
