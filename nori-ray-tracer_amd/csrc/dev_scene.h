@@ -85,9 +85,11 @@ struct DevScene {
     float sigma_t[3], albedo[3];
     // Small scenes: every table above packed into one blob (byte offsets),
     // which latency-bound kernels stage into LDS (blob_bytes == 0: none).
-    // photonmapper: photons (position, direction, power; 3 float4 each) sorted
-    // by hash-grid bucket, bucket starts (ph_mask + 2 entries), cell size r
-    const float4 *ph;
+    // photonmapper: photons sorted by hash-grid bucket, bucket starts
+    // (ph_mask + 2 entries), cell size r
+    const float4 *ph;            // (x, y, z, theta | phi << 8 as bits): 16 B read per candidate
+    const uint32_t *ph_rgbe;     // r | g << 8 | b << 16 | e << 24, read for photons inside the radius
+    const float *ph_tab;         // PhotonData tables: cos phi, sin phi, cos theta, sin theta, exp (5 x 256)
     const uint32_t *ph_start;
     uint32_t ph_mask;
     float ph_inv_cell, ph_r2, ph_norm;  // 1/r, r*r, r*r*photonCount (photonmapper.cpp:177)

@@ -90,10 +90,12 @@ struct DeviceBvh {
 void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const float root_max[3], DeviceBvh &out);
 
 // Photon map (photon_map.cpp): raw = n photons x 12 floats (position, 0,
-// direction towards the light, 0, power, 0) in emission order -> the same
-// layout after the reference's PhotonData quantization, sorted by hash-grid
-// bucket of cell size `radius`; start = bucket offsets (mask + 2 entries).
+// direction towards the light, 0, power, 0) in emission order -> photons as
+// (x, y, z, theta | phi << 8) and RGBE words (the reference's PhotonData),
+// sorted by hash-grid bucket of cell size `radius`; tables = PhotonData's
+// 5 x 256 decode tables; start = bucket offsets (mask + 2 entries).
 void build_photon_map(const std::vector<float> &raw, uint32_t n, float radius, std::vector<float> &photons,
-                      std::vector<uint32_t> &start, uint32_t &mask);
+                      std::vector<uint32_t> &rgbe, std::vector<float> &tables, std::vector<uint32_t> &start,
+                      uint32_t &mask);
 
 }  // namespace nori

@@ -1928,18 +1928,28 @@ struct OneBounce {
                             const uint32_t h = photon_cell_hash(gx, gy, gz) & S.ph_mask;
                             const uint32_t j1 = S.ph_start[h + 1];
                             for (uint32_t j = S.ph_start[h]; j < j1; ++j) {
-                                const float4 pp = gld(S.ph + 3 * (size_t)j);
+                                const float4 pp = gld(S.ph + j);
+                                const V3 dd = ld3(pp) - hs.p;
+                                if (!(dot(dd, dd) < S.ph_r2)) continue;
+                                // own cell only (a bucket may hold colliding cells)
                                 if ((int)floorf(pp.x * ic) != gx || (int)floorf(pp.y * ic) != gy ||
                                     (int)floorf(pp.z * ic) != gz)
                                     continue;
-                                const V3 dd = ld3(pp) - hs.p;
-                                if (!(dot(dd, dd) < S.ph_r2)) continue;
                                 BRec br;
                                 br.wi = wi;
-                                br.wo = to_local(hs.sh, ld3(gld(S.ph + 3 * (size_t)j + 1)));
+                                // PhotonData::getDirection / getPower (photon.h:44-55)
+                                const uint32_t dir = __float_as_uint(pp.w), rgbe = S.ph_rgbe[j];
+                                const float *T = S.ph_tab;
+                                const float st = T[768 + (dir & 255u)];
+                                const V3 wd{T[(dir >> 8) & 255u] * st, T[256 + ((dir >> 8) & 255u)] * st,
+                                            T[512 + (dir & 255u)]};
+                                const float sc = T[1024 + (rgbe >> 24)];
+                                const V3 pw{(float)(rgbe & 255u) * sc, (float)((rgbe >> 8) & 255u) * sc,
+                                            (float)((rgbe >> 16) & 255u) * sc};
+                                br.wo = to_local(hs.sh, wd);
                                 br.measure = kMeasureSolidAngle;
                                 br.uv = hs.uv;
-                                pc = pc + bsdf_eval(B, br) * ld3(gld(S.ph + 3 * (size_t)j + 2));
+                                pc = pc + bsdf_eval(B, br) * pw;
                             }
                         }
                 return color + att * ((pc * kInvPi) / S.ph_norm);

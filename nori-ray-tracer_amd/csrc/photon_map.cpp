@@ -5,7 +5,8 @@
 // (photon.h, photon.cpp:30-74): the direction quantized to 8-bit spherical
 // angles and the power in Ward's RGBE, decoded through the same 256-entry
 // tables -- so the density estimate sums exactly the reference's photon
-// values.  The reference's kd-tree (kdtree.h) answers "every photon with
+// values (the device decodes the packed angles and RGBE through the same
+// tables, so only 16 bytes per candidate photon are read).  The reference's kd-tree (kdtree.h) answers "every photon with
 // |x - p|^2 < r^2"; here a hash grid of cell size r answers the same query
 // from the 27 cells around p (kernels.hip, OneBounce::Li_pmap).
 #include <algorithm>
@@ -43,10 +44,18 @@ uint32_t cell_hash(const float *p, float ic) {  // == kernels.hip: (int)floorf(p
 }  // namespace
 
 void build_photon_map(const std::vector<float> &raw, uint32_t n, float radius, std::vector<float> &photons,
-                      std::vector<uint32_t> &start, uint32_t &mask) {
+                      std::vector<uint32_t> &rgbe_out, std::vector<float> &tables, std::vector<uint32_t> &start,
+                      uint32_t &mask) {
     static const PhotonTables T;
-    // PhotonData(dir, power) (photon.cpp:43-74) and getDirection / getPower (photon.h:44-55)
-    std::vector<float> dec(12 * (size_t)n);
+    tables.assign(5 * 256, 0.0f);
+    for (int i = 0; i < 256; ++i) {
+        tables[i] = T.cos_phi[i], tables[256 + i] = T.sin_phi[i], tables[512 + i] = T.cos_theta[i];
+        tables[768 + i] = T.sin_theta[i], tables[1024 + i] = T.exp_table[i];
+    }
+    // PhotonData(dir, power) (photon.cpp:43-74); the device decodes it as
+    // getDirection / getPower (photon.h:44-55) through the same tables
+    std::vector<float> dec(4 * (size_t)n);
+    std::vector<uint32_t> code(n);
     for (uint32_t i = 0; i < n; ++i) {
         const float *r = &raw[12 * (size_t)i];
         const float dx = r[4], dy = r[5], dz = r[6];
@@ -67,13 +76,11 @@ void build_photon_map(const std::vector<float> &raw, uint32_t n, float radius, s
             rgbe[2] = (uint8_t)(pb * mx);
             rgbe[3] = (uint8_t)(e + 128);
         }
-        float *d = &dec[12 * (size_t)i];
-        d[0] = r[0], d[1] = r[1], d[2] = r[2], d[3] = 0;
-        d[4] = T.cos_phi[phi] * T.sin_theta[theta];
-        d[5] = T.sin_phi[phi] * T.sin_theta[theta];
-        d[6] = T.cos_theta[theta], d[7] = 0;
-        const float s = T.exp_table[rgbe[3]];
-        d[8] = (float)rgbe[0] * s, d[9] = (float)rgbe[1] * s, d[10] = (float)rgbe[2] * s, d[11] = 0;
+        float *d = &dec[4 * (size_t)i];
+        const uint32_t dir = (uint32_t)theta | ((uint32_t)phi << 8);
+        d[0] = r[0], d[1] = r[1], d[2] = r[2];
+        std::memcpy(&d[3], &dir, 4);
+        code[i] = (uint32_t)rgbe[0] | ((uint32_t)rgbe[1] << 8) | ((uint32_t)rgbe[2] << 16) | ((uint32_t)rgbe[3] << 24);
     }
     // hash grid: buckets = the power of two >= 2n, photons sorted by bucket
     uint32_t buckets = 1024;
@@ -83,15 +90,19 @@ void build_photon_map(const std::vector<float> &raw, uint32_t n, float radius, s
     std::vector<uint32_t> key(n);
     start.assign((size_t)buckets + 2, 0);
     for (uint32_t i = 0; i < n; ++i) {
-        key[i] = cell_hash(&dec[12 * (size_t)i], ic) & mask;
+        key[i] = cell_hash(&dec[4 * (size_t)i], ic) & mask;
         ++start[key[i] + 1];
     }
     for (uint32_t b = 0; b < buckets; ++b) start[b + 1] += start[b];
     start[(size_t)buckets + 1] = start[buckets];
     std::vector<uint32_t> fill(start.begin(), start.begin() + buckets);
-    photons.assign(12 * (size_t)n, 0.0f);
-    for (uint32_t i = 0; i < n; ++i)  // stable: emission order within a bucket
-        std::memcpy(&photons[12 * (size_t)fill[key[i]]++], &dec[12 * (size_t)i], 12 * sizeof(float));
+    photons.assign(4 * (size_t)n, 0.0f);
+    rgbe_out.assign(n, 0u);
+    for (uint32_t i = 0; i < n; ++i) {  // stable: emission order within a bucket
+        const uint32_t at = fill[key[i]]++;
+        std::memcpy(&photons[4 * (size_t)at], &dec[4 * (size_t)i], 4 * sizeof(float));
+        rgbe_out[at] = code[i];
+    }
 }
 
 }  // namespace nori

@@ -201,7 +201,7 @@ struct nori_gpu_ctx {
     DevBuf q[2][6], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
     DevBuf ptctr;                    // persistent traversal work counters, 4 per part
     DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
-    DevBuf ph, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
+    DevBuf ph, ph_rgbe, ph_tab, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
     uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
@@ -739,13 +739,17 @@ void photon_preprocess(nori_gpu_ctx &c, const nori_scene_desc &d) {
     HIP_TRY(launch_photons(c.S, 0, (uint32_t)pre.size(), nullptr, dpre.as<uint64_t>(), N, out.as<float4>(), c.stack,
                            c.stream));
     HIP_TRY(hipStreamSynchronize(c.stream));
-    std::vector<float> raw(12 * (size_t)N), ph;
+    std::vector<float> raw(12 * (size_t)N), ph, tab;
     HIP_TRY(hipMemcpy(raw.data(), out.p, 48 * (size_t)N, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> start;
+    std::vector<uint32_t> start, rgbe;
     uint32_t mask = 0;
-    build_photon_map(raw, (uint32_t)N, d.photon_radius, ph, start, mask);
+    build_photon_map(raw, (uint32_t)N, d.photon_radius, ph, rgbe, tab, start, mask);
     c.ph.upload(ph);
+    c.ph_rgbe.upload(rgbe);
+    c.ph_tab.upload(tab);
     c.ph_start.upload(start);
+    c.S.ph_rgbe = c.ph_rgbe.as<uint32_t>();
+    c.S.ph_tab = c.ph_tab.as<float>();
     const float r = d.photon_radius;
     c.S.ph = c.ph.as<float4>();
     c.S.ph_start = c.ph_start.as<uint32_t>();
