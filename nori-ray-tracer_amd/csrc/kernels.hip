@@ -1927,8 +1927,19 @@ struct OneBounce {
                             const int gx = cx + dx, gy = cy + dy, gz = cz + dz;
                             const uint32_t h = photon_cell_hash(gx, gy, gz) & S.ph_mask;
                             const uint32_t j1 = S.ph_start[h + 1];
-                            for (uint32_t j = S.ph_start[h]; j < j1; ++j) {
-                                const float4 pp = gld(S.ph + j);
+#ifndef NORI_PMAP_BATCH
+#define NORI_PMAP_BATCH 4  // candidate photons whose positions are loaded together
+#endif
+                            for (uint32_t j0 = S.ph_start[h]; j0 < j1; j0 += NORI_PMAP_BATCH) {
+                              float4 qb[NORI_PMAP_BATCH];
+#pragma unroll
+                              for (int u = 0; u < NORI_PMAP_BATCH; ++u)
+                                  qb[u] = j0 + u < j1 ? gld(S.ph + j0 + u) : make_float4(0, 0, 0, 0);
+#pragma unroll
+                              for (int u = 0; u < NORI_PMAP_BATCH; ++u) {
+                                const uint32_t j = j0 + u;
+                                if (j >= j1) break;
+                                const float4 pp = qb[u];
                                 const V3 dd = ld3(pp) - hs.p;
                                 if (!(dot(dd, dd) < S.ph_r2)) continue;
                                 // own cell only (a bucket may hold colliding cells)
@@ -1950,6 +1961,7 @@ struct OneBounce {
                                 br.measure = kMeasureSolidAngle;
                                 br.uv = hs.uv;
                                 pc = pc + bsdf_eval(B, br) * pw;
+                              }
                             }
                         }
                 return color + att * ((pc * kInvPi) / S.ph_norm);
