@@ -46,6 +46,8 @@ __global__ __launch_bounds__(256) void k_nlmeans(const float *__restrict__ img, 
     float *A = lds;                   // AW x AH x 4 (r, g, b, variance)
     float *D = A + 4 * AW * AH;       // DW x DH
     float *G = D + DW * DH;           // GW x GH
+    float *Hs = G + GW * GH;          // DH x GW: row sums of D (first box, separable)
+    float *Hg = D;                    // GH x kDnTX: row sums of G (second box; D is free by then)
     const int x0 = blockIdx.x * kDnTX, y0 = blockIdx.y * kDnTY, tid = threadIdx.x;
     for (int i = tid; i < AW * AH; i += 256) {
         const int ay = i / AW, ax = i - ay * AW;
@@ -87,26 +89,39 @@ __global__ __launch_bounds__(256) void k_nlmeans(const float *__restrict__ img, 
                 D[i] = d2;
             }
             __syncthreads();
-            // wgt = exp(-max(0, box(d2pixel))) on the tile +- p, zero outside the image
+            // box means as row sums then column sums (separable, zero outside the image)
+            for (int i = tid; i < DH * GW; i += 256) {
+                const int y = i / GW, x = i - y * GW;
+                float r = 0.0f;
+                for (int l = 0; l <= 2 * P; ++l) r += D[y * DW + x + l];
+                Hs[i] = r;
+            }
+            __syncthreads();
+            // wgt = exp(-max(0, box(d2pixel))) on the tile +- p
             for (int i = tid; i < GW * GH; i += 256) {
                 const int gy = i / GW, gx = i - gy * GW;
                 const int y = y0 - P + gy, x = x0 - P + gx;
                 float w = 0.0f;
                 if (y >= 0 && y < H && x >= 0 && x < W) {
-                    float s = 0.0f;
-                    for (int j = 0; j <= 2 * P; ++j)
-                        for (int l = 0; l <= 2 * P; ++l) s += D[(gy + j) * DW + gx + l];
-                    w = expf(-fmaxf(0.0f, s * inv_box));
+                    float c = 0.0f;
+                    for (int j = 0; j <= 2 * P; ++j) c += Hs[(gy + j) * GW + gx];
+                    w = expf(-fmaxf(0.0f, c * inv_box));
                 }
                 G[i] = w;
             }
             __syncthreads();
+            for (int i = tid; i < GH * kDnTX; i += 256) {
+                const int y = i / kDnTX, x = i - y * kDnTX;
+                float r = 0.0f;
+                for (int l = 0; l <= 2 * P; ++l) r += G[y * GW + x + l];
+                Hg[i] = r;
+            }
+            __syncthreads();
             for (int h = 0; h < 2; ++h) {
                 const int t = tid + 256 * h, ty = t / kDnTX, tx = t - ty * kDnTX;
-                float s = 0.0f;
-                for (int j = 0; j <= 2 * P; ++j)
-                    for (int l = 0; l <= 2 * P; ++l) s += G[(ty + j) * GW + tx + l];
-                const float w = s * inv_box;
+                float c = 0.0f;
+                for (int j = 0; j <= 2 * P; ++j) c += Hg[(ty + j) * kDnTX + tx];
+                const float w = c * inv_box;
                 const float *q = A + 4 * ((ty + halo - sr) * AW + (tx + halo - sc));
                 acc[h][0] += w * q[0];
                 acc[h][1] += w * q[1];
@@ -132,7 +147,8 @@ __global__ __launch_bounds__(256) void k_nlmeans(const float *__restrict__ img, 
 size_t denoise_lds_bytes(int R, int P) {
     const int halo = R + 2 * P;
     return sizeof(float) * ((size_t)4 * (kDnTX + 2 * halo) * (kDnTY + 2 * halo) +
-                            (size_t)(kDnTX + 4 * P) * (kDnTY + 4 * P) + (size_t)(kDnTX + 2 * P) * (kDnTY + 2 * P));
+                            (size_t)(kDnTX + 4 * P) * (kDnTY + 4 * P) + (size_t)(kDnTX + 2 * P) * (kDnTY + 2 * P) +
+                            (size_t)(kDnTY + 4 * P) * (kDnTX + 2 * P));
 }
 
 hipError_t launch_denoise(const float *img, const float *var, int W, int H, int R, int P, float k, int mode,
