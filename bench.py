@@ -1,34 +1,43 @@
 """Headline benchmark: Msamples/s on cbox_path_mis 512x512 @ 512 spp.
 
-A step = one full render of the workload (512x512 pixels x 512 sample passes
-= 134,217,728 camera samples of path_mis, scenes/pa4/cbox/cbox_path_mis.xml
-with its mirror and dielectric spheres) from resident scene data to the
-filtered RGBW film in HBM.
+A step = one full render of the workload (default: 512x512 pixels x 512
+sample passes = 134,217,728 camera samples of path_mis on
+scenes/pa4/cbox/cbox_path_mis.xml, with its mirror and dielectric spheres),
+from resident scene data to the filtered RGBW film in HBM.  --config c3|c4|c5
+benches the other single-GPU-sized BASELINE configs (nori_amd.configs).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU; rank r renders the disjoint sample passes [r*spp, (r+1)*spp) of the
-same frame (weak scaling: per-GPU work is fixed) and the RGBW films are summed
-over RCCL (all_reduce) -- the reference's ImageBlock::put(block) merge
-(block.cpp:124-133).  value = samples of all ranks / max-over-ranks time.
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one
+process per GPU.  STRONG scaling: the frame is fixed and split over the ranks
+by libnori_gpu itself (nori_gpu_render_sharded: rank r renders sample passes
+[P r/N, P (r+1)/N), or --shard blocks: every N-th 32x32 block of the spiral
+order), and the library sums the RGBW films into rank 0 with RCCL over xGMI --
+the reference's ImageBlock::put(block) merge (block.cpp:124-133).  The step
+time includes that sum.  value = the frame's samples / max-over-ranks time.
+torch.distributed (gloo) only carries the communicator id, the barriers and
+the max of the rank times.
 
 Extra fields:
-  roofline     -- the dominant kernel (most HIP-event time in the last timed
-                  step; k_shade on this workload): algorithmic HBM bytes per
-                  launch over its average launch time against the 8 TB/s HBM
-                  peak (launch times inside the timed region, where two pool
-                  parts on two streams share the chip; `isolated_frac` uses the
-                  serialised launch time of the committed counter passes), `traffic` = measured HBM bytes per launch from the
-                  committed rocprofv3 PMC summary (profiles/pmc_r01.json), and
-                  a per-kernel table (the traversal kernels are VALU-bound:
-                  VALU issue rate against the issue peak).
+  roofline     -- the traversal kernel k_extend (north_star's target) against
+                  the 8 TB/s HBM peak: algorithmic bytes per launch (48 B per
+                  extension ray + the scene's primitive/node bytes, SURVEY.md
+                  8(d)) over its average launch time, from HIP events in an
+                  extra render after the timed region with ONE pool part (the
+                  timed renders run two parts on two streams, so a kernel's
+                  event time there includes the other part's kernels);
+                  `traffic` = measured HBM bytes per launch of the committed
+                  rocprofv3 counter passes of `bench.py --roofline-only`
+                  (profiles/).  `kernels` holds k_shade / k_shadow alike.
   cpu_baseline -- the CPU oracle (reference structure: sample-outer passes,
-                  32x32 blocks, per-block pcg32 streams) timed on this host on
-                  a bounded sample of the same workload (rank 0, N=1 only).
+                  32x32 blocks, per-block pcg32 streams, serial variance
+                  sweep) timed on this host's usable cores on a bounded
+                  number of passes of the same workload (rank 0, N=1 only).
 """
 import argparse
 import json
+import math
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -37,10 +46,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "nori-ray-tracer_amd"))
 
 import nori_amd  # noqa: E402
+from nori_amd import configs  # noqa: E402
+from nori_amd import distributed as nd  # noqa: E402
+from nori_amd._abi import BLOCK_SIZE  # noqa: E402
 
 METRIC = "Msamples/sec on cbox_path_mis 512×512@512spp; per-pixel L2 vs CPU ref"
-SCENE = os.path.join(ROOT, "scenes", "pa4", "cbox", "cbox_path_mis.xml")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PROFILE = os.path.join(ROOT, "profiles", "pmc_r02.json")  # committed rocprofv3 evidence (tools/pmc_to_profile.py)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2 * 64  # lane-instr/s: 256 CUs x 4 SIMDs, a wave64 VALU op per 2 cycles
 
 
 def cpu_model():
@@ -53,13 +66,27 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(width, height, target_s):
+def usable_cpus():
+    """(threads used, affinity-mask CPUs, cgroup CPU quota or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return threads, aff, quota
+
+
+def cpu_baseline(xml, width, height, target_s):
     """Oracle in reference (BLOCK stream) mode on a bounded number of passes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    threads = min(16, os.cpu_count() or 1)
-    scene = nori_amd.load_scene(SCENE, width, height, 1)
+    threads, aff, quota = usable_cpus()
+    scene = nori_amd.load_scene(xml, width, height, 1)
     o = pyoracle.OracleScene(scene)
     o.render(passes=1, rng="block", threads=threads, variance_pass=True)
     t1 = o.last_stats["ms_render"] / 1e3
@@ -73,24 +100,22 @@ def cpu_baseline(width, height, target_s):
         "kind": "port",
         "sample": f"{width}x{height} x {passes} passes of the same scene ({st['samples']} samples, "
                   f"{st['ms_render'] / 1e3:.1f} s), reference stream layout, serial variance pass included; "
-                  f"CPU: {cpu_model()}",
+                  f"{st['threads']} threads = the process's usable CPUs (affinity mask {aff}, cgroup quota "
+                  f"{quota if quota is not None else 'none'}); CPU: {cpu_model()}",
     }
 
 
-def parity_check():
-    """Small-size per-pixel L2 of the GPU image against the oracle (same streams)."""
+def parity_check(xml, width, height, spp):
+    """Per-pixel L2 of the GPU image against the oracle on identical WAVE streams."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    s = nori_amd.load_scene(SCENE, 128, 128, 16)
+    s = nori_amd.load_scene(xml, width, height, spp)
     with nori_amd.GpuRenderer(s, 0) as r:
         gpu = nori_amd.develop(s, r.render())
-    cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
-    return {"l2": float(np.mean((gpu - cpu) ** 2)), "config": "128x128@16spp, identical WAVE streams"}
-
-
-PROFILE = os.path.join(ROOT, "profiles", "pmc_r01.json")  # committed rocprofv3 evidence (tools/pmc_to_profile.py)
-VALU_PEAK = 256 * 4 * 2.4e9 / 2 * 64  # lane-instr/s: 256 CUs x 4 SIMDs, a wave64 VALU op per 2 cycles
+    cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave", threads=usable_cpus()[0]))
+    return {"l2": float(np.mean((gpu - cpu) ** 2)), "tolerance": 1e-3,
+            "config": f"{width}x{height}@{spp}spp of the benched scene, identical WAVE streams"}
 
 
 def profiled(prefix):
@@ -106,55 +131,51 @@ def profiled(prefix):
 
 
 def roofline(ts, samples):
-    """Roofline of the dominant kernel (most HIP-event time) of the timing render.
+    """Per-kernel roofline rows of an isolated (one pool part) timing render.
 
-    Algorithmic HBM bytes per kernel:
+    Algorithmic HBM bytes:
+      k_extend: per extension ray read ray_o, ray_d (32 B), write hit (16 B);
+                plus the scene's node + primitive bytes once per launch
+      k_shadow: per shadow ray read ray_o, ray_d, payload (48 B) (+ the scene)
       k_shade : per path read ray_o, ray_d, thr, rng, hit (16 B each) + work (4 B) = 84 B,
                 per surviving path write ray_o, ray_d, thr, rng + work = 68 B,
-                per shadow ray 48 B (origin, direction, payload), per new sample 16 B
-                record + 4 B pixel index
-      k_extend: per ray read ray_o, ray_d (32 B), write hit (16 B)
-      k_shadow: per shadow ray read ray_o, ray_d, payload (48 B)
-    The traversal kernels are VALU-bound (scan over the primitive list); their
-    VALU issue rate (SQ_INSTS_VALU x 64 lanes per launch, rocprofv3) is given
-    against the issue peak.
+                per shadow ray 48 B, per new sample 16 B record + 4 B pixel index
     """
-    launches = max(ts["iterations"] * max(ts.get("stream_parts", 1), 1), 1)  # per kernel
-    rc, rs = ts["rays_closest"], ts["rays_shadow"]
+    launches = max(ts["iterations"] * max(ts.get("stream_parts", 1), 1), 1)
+    rc, rs, scene = ts["rays_closest"], ts["rays_shadow"], ts["scene_bytes"]
     kern = {
-        "shade": ("k_shade", ts["ms_shade"], rc * (84 + 68) + rs * 48 + samples * 20),
-        "extend": ("k_extend", ts["ms_extend"], rc * 48),
-        "shadow": ("k_shadow", ts["ms_shadow"], rs * 48),
+        "k_extend": (ts["ms_extend"], rc * 48 + scene * launches),
+        "k_shadow": (ts["ms_shadow"], rs * 48 + scene * launches),
+        "k_shade": (ts["ms_shade"], rc * (84 + 68) + rs * 48 + samples * 20),
     }
     rows = {}
-    for key, (name, ms, nbytes) in kern.items():
+    for name, (ms, nbytes) in kern.items():
         if ms <= 0:
             continue
-        prof = profiled(name)
         avg = ms / launches
-        row = {"ms": ms, "avg_launch_ms": avg, "bytes_per_launch": nbytes / launches,
+        row = {"ms_per_step": ms, "launches": launches, "avg_launch_ms": avg, "bytes_per_launch": nbytes / launches,
                "achieved_GBs": nbytes / launches / (avg / 1e3) / 1e9}
+        row["frac"] = row["achieved_GBs"] / HBM_PEAK_GBS
+        prof = profiled(name)
         if prof:
             row["traffic_bytes_per_launch"] = prof.get("hbm_bytes_per_launch")
             row["rocprof_avg_launch_ms"] = prof.get("trace_avg_ms")
-            # the counter passes serialise the kernels: this launch time has no
-            # second stream beside it (the timed region overlaps two pool parts)
-            iso = prof.get("profiled_ms_per_launch")
-            if iso:
-                row["isolated_launch_ms"] = iso
-                row["isolated_achieved_GBs"] = nbytes / launches / (iso / 1e3) / 1e9
             if prof.get("sq_insts_valu_per_launch") and prof.get("trace_avg_ms"):
                 rate = prof["sq_insts_valu_per_launch"] * 64 / (prof["trace_avg_ms"] / 1e3)
-                row["valu_lane_instr_per_s"] = rate
                 row["valu_issue_frac"] = rate / VALU_PEAK
         rows[name] = row
-    dom = max(rows, key=lambda k: rows[k]["ms"])
-    d = rows[dom]
-    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": d["achieved_GBs"] / HBM_PEAK_GBS, "traffic": d.get("traffic_bytes_per_launch"),
-            "isolated_frac": (d["isolated_achieved_GBs"] / HBM_PEAK_GBS) if "isolated_achieved_GBs" in d else None,
+    d = rows["k_extend"]
+    return {"bound": "hbm", "kernel": "k_extend", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": d["frac"], "traffic": d.get("traffic_bytes_per_launch"),
             "bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": d["avg_launch_ms"], "launches": launches,
-            "kernels": rows}
+            "measured": "HIP events on the launch stream, one extra render after the timed region with one pool "
+                        "part (NORI_POOL_PARTS=1): kernels serialised on one stream",
+            "ms_per_step_isolated": ts["ms_total"], "kernels": rows}
+
+
+def hip_runtime():
+    libs = sorted({l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l})
+    return libs
 
 
 def main():
@@ -165,75 +186,104 @@ def main():
     # (tools/step_times.py); from the third on the step time is steady
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=512)
-    ap.add_argument("--height", type=int, default=512)
-    ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--config", default="c2", choices=sorted(configs.CONFIGS))
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
+    ap.add_argument("--shard", default="passes", choices=["passes", "blocks"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="profiling helper: one warm-up and one measuring render with one pool part "
+                         "(the render bench.py's roofline times), then exit")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    tmp = tempfile.mkdtemp(prefix="nori_bench_")
+    xml, label, W, H, spp = configs.config_scene(args.config, tmp, args.width, args.height, args.spp)
+    scene = nori_amd.load_scene(xml, W, H, spp)
+    r = nori_amd.GpuRenderer(scene, local)
+
+    if args.roofline_only:
+        os.environ["NORI_POOL_PARTS"] = "1"
+        r.render(path_pool=args.pool)
+        r.render(path_pool=args.pool, timing=True)
+        print(json.dumps({"roofline_only": True, "workload": label, "stats": r.last_stats}), flush=True)
+        r.close()
+        return
+
+    import torch
+
     dist = None
-    torch = None
+    comm = None
     if world > 1:
-        import torch
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-
-    scene = nori_amd.load_scene(SCENE, args.width, args.height, args.spp)
-    r = nori_amd.GpuRenderer(scene, local)
-    film_shape = scene.film_shape()
-    film_t = None
-    if world > 1:
-        film_t = torch.zeros(film_shape, dtype=torch.float32, device=f"cuda:{local}")
+        dist.init_process_group(backend="gloo")
+        comm = nd.film_comm(dist, local)
+    film = torch.zeros(scene.film_shape(), dtype=torch.float32, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+    share = nd.shard(scene, rank, world, args.shard) if world > 1 else (0, spp, None)
+    nbx = -(-W // BLOCK_SIZE)
+    share_samples = share[1] * (W * H if share[2] is None else sum(
+        min(BLOCK_SIZE, W - (b % nbx) * BLOCK_SIZE) *
+        min(BLOCK_SIZE, H - (b // nbx) * BLOCK_SIZE) for b in share[2]))
 
     def step(timing=False):
         if world > 1:
-            from nori_amd import distributed as nd
-
-            film_t.zero_()
-            torch.cuda.synchronize()
-            pb, pc = nd.pass_range(rank, args.spp)
-            r.render(passes=pc, pass_begin=pb, device_ptr=film_t.data_ptr(), path_pool=args.pool, timing=timing)
-            nd.reduce_film(film_t, dist)
+            r.render_sharded(comm, film.data_ptr(), mode=args.shard, root=0, path_pool=args.pool, timing=timing)
         else:
-            r.render(passes=args.spp, path_pool=args.pool, timing=timing)
-        return r.last_stats
+            film.zero_()
+            torch.cuda.synchronize()
+            r.render(passes=spp, path_pool=args.pool, device_ptr=film.data_ptr(), timing=timing)
+        st = r.last_stats
+        assert st["samples"] == share_samples, (st["samples"], share_samples)
+        return st
 
     def sync():
+        torch.cuda.synchronize()
         if world > 1:
-            torch.cuda.synchronize()
             dist.barrier()
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
     sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        # the last timed step also records HIP events around every kernel (on
-        # the renderer's stream) for the per-kernel times of the roofline;
-        # their small overhead stays inside the timed region
-        ts = step(timing=(i == args.steps - 1))
+    invalid = 0
+    for _ in range(args.steps):
+        invalid += step()["invalid_samples"]
     sync()
     elapsed = time.perf_counter() - t0
+    last = r.last_stats
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    samples_per_step = args.width * args.height * args.spp
-    value = world * samples_per_step * args.steps / elapsed / 1e6
+    samples_per_step = W * H * spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        os.environ["NORI_POOL_PARTS"] = "1"
+        r.render(passes=share[1], pass_begin=share[0], blocks=share[2], path_pool=args.pool)
+        r.render(passes=share[1], pass_begin=share[0], blocks=share[2], path_pool=args.pool, timing=True)
+        ts = r.last_stats
+        os.environ.pop("NORI_POOL_PARTS")
+        roof = roofline(ts, share_samples)
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == "c2" else f"Msamples/sec on {label}",
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -241,31 +291,40 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: the reference's cbox_path_mis scene file, no external assets",
-            "config": {"workload": f"cbox_path_mis {args.width}x{args.height}@{args.spp}spp",
-                       "scene": "scenes/pa4/cbox/cbox_path_mis.xml", "integrator": "path_mis",
-                       "parallelism": f"pass-range sharding x{world}, RCCL film all_reduce" if world > 1
+            "data": "synthetic: the reference's scene files (C3/C4: generated mesh / env map, nori_amd.configs)",
+            "config": {"workload": label, "scene": os.path.relpath(xml, ROOT) if xml.startswith(ROOT) else
+                       os.path.basename(xml), "integrator": scene.integrator,
+                       "parallelism": f"{args.shard}-sharded x{world}, RCCL film reduce in libnori_gpu" if world > 1
                        else "single GPU", "path_pool": args.pool or 4194304},
-            "roofline": roofline(ts, samples_per_step),
-            "kernel_ms": {"extend": ts["ms_extend"], "shadow": ts["ms_shadow"], "shade": ts["ms_shade"],
-                          "splat": ts["ms_splat"], "finish": ts["ms_finish"], "wall": ts["ms_total"]},
-            "rays_per_sample": {"closest": ts["rays_closest"] / samples_per_step,
-                                "shadow": ts["rays_shadow"] / samples_per_step,
-                                "finisher": ts["rays_finish"] / samples_per_step},
-            "wavefront_iterations": ts["iterations"],
-            "stream_parts": ts.get("stream_parts", 1),
+            "samples_per_step": samples_per_step,
+            "invalid_samples": invalid,
+            "roofline": roof,
+            "kernel_ms_isolated": {k: roof["kernels"][k]["ms_per_step"] for k in roof["kernels"]} if roof else None,
+            "rays_per_sample": {"closest": last["rays_closest"] / share_samples,
+                                "shadow": last["rays_shadow"] / share_samples,
+                                "finisher": last["rays_finish"] / share_samples},
+            "wavefront_iterations": last["iterations"],
+            "stream_parts": last.get("stream_parts", 1),
+            "hip_runtime": hip_runtime(),
         }
         if world == 1 and not args.no_parity:
-            out["parity"] = parity_check()
+            small = {"c2": (512, 512, 16), "c3": (128, 128, 4), "c4": (128, 128, 8), "c5": (160, 120, 8)}
+            pw, ph, ps = small[args.config]
+            pxml = xml if args.config != "c3" else configs.heightfield_scene(tmp, n=512, width=pw, height=ph, spp=ps)
+            if args.config == "c4":
+                pxml = configs.envmap_scene(tmp, pw, ph, ps)
+            out["parity"] = parity_check(pxml, pw, ph, ps)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.width, args.height, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(xml, W, H, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     r.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

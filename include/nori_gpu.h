@@ -26,6 +26,11 @@
  *   nori_film_variance    <- renderScene's variance image src/render.cpp:164-169,190-245
  *   nori_denoise          <- denoiser/denoiser.py:53-66 (NL-means)
  *   nori_scene_bvh_info   <- BVH::build/statistics        src/bvh.cpp:329-402
+ *   nori_gpu_comm_*, nori_gpu_render_sharded
+ *                         <- the same pass loop spread over the GPUs of a node,
+ *                            one process per GPU; the cross-GPU film merge is
+ *                            ImageBlock::put(block) src/block.cpp:124-133 as an
+ *                            RCCL sum over xGMI (the reference has no multi-device path)
  *
  * Rules of the ABI: plain C types only, no exceptions cross it, every call
  * returns an int status (NORI_OK = 0, negative = error) and the message of
@@ -316,6 +321,44 @@ int nori_gpu_trace(nori_gpu_ctx *ctx, const float *rays, uint32_t n, int any_hit
 int nori_gpu_cancel(nori_gpu_ctx *ctx);
 float nori_gpu_progress(const nori_gpu_ctx *ctx);
 void nori_gpu_destroy(nori_gpu_ctx *ctx);
+
+/* ---- multi-GPU: one process per GPU, film sum over RCCL -------------------
+ * Samples are independent, so a frame shards without any data-path
+ * collective; the only exchange is the final film sum.  librccl is opened at
+ * run time from the directory of the process's HIP runtime (fallback:
+ * librccl.so.1); without it these calls fail with NORI_ERR_UNSUPPORTED and
+ * everything else works. */
+typedef struct nori_gpu_comm nori_gpu_comm;
+#define NORI_COMM_ID_BYTES 128
+/* Rank 0 makes the communicator id (ncclGetUniqueId); the caller hands the
+ * bytes to every rank over any channel (torch.distributed store, MPI, file). */
+int nori_gpu_comm_id(unsigned char id[NORI_COMM_ID_BYTES]);
+/* Collective over the nranks processes (ncclCommInitRank); device = this
+ * process's GPU (the device of the contexts used with the communicator). */
+int nori_gpu_comm_create(const unsigned char id[NORI_COMM_ID_BYTES], int nranks, int rank, int device,
+                         nori_gpu_comm **out);
+int nori_gpu_comm_rank(const nori_gpu_comm *comm, int *nranks, int *rank);
+void nori_gpu_comm_destroy(nori_gpu_comm *comm);
+/* Path of the librccl opened (loading it if needed), NULL if none loads. */
+const char *nori_gpu_comm_library(void);
+
+#define NORI_SHARD_PASSES 0  /* rank r: passes [P*r/N, P*(r+1)/N) of every block (default) */
+#define NORI_SHARD_BLOCKS 1  /* rank r: blocks r, r+N, r+2N, ... of the BlockGenerator's spiral
+                                order (block.cpp:140-188), every pass */
+/* The share of a whole-frame render `desc` that rank `rank` of `nranks`
+ * renders: writes this rank's pass range and (BLOCKS) block ids into *out and
+ * block_buf (capacity = the frame's block count).  desc->num_blocks != 0
+ * restricts the frame to those blocks first.  out->pass_count == 0: the rank
+ * has no share (more ranks than passes / blocks).  Pure host function. */
+int nori_gpu_shard_desc(const nori_scene_desc *scene, const nori_gpu_render_desc *desc, int mode, int nranks,
+                        int rank, nori_gpu_render_desc *out, uint32_t *block_buf);
+/* Render this rank's share of `desc` into film_dev (device memory on the
+ * context's device, (H+2b)x(W+2b)x4 floats; ZEROED first) and sum the films
+ * of all ranks on the context's stream: into root's film_dev (ncclReduce), or
+ * into every rank's when root < 0 (ncclAllReduce).  Returns after the sum has
+ * completed on this rank.  stats: this rank's share. */
+int nori_gpu_render_sharded(nori_gpu_ctx *ctx, nori_gpu_comm *comm, const nori_gpu_render_desc *desc, int mode,
+                            int root, float *film_dev, nori_gpu_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.h"
 #include "host_scene.h"
 #include "kernels.h"
 
@@ -192,6 +193,7 @@ struct nori_gpu_ctx {
     DevScene S{};
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob;
+    uint32_t spp = 1;    // the scene's sampleCount (default pass count)
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
     uint32_t bvh_depth = 0, bvh_nodes = 0, num_prims = 0;
     size_t scene_bytes = 0;
@@ -220,6 +222,12 @@ struct nori_gpu_ctx {
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
+};
+
+struct nori_gpu_comm {
+    void *nccl = nullptr;  // ncclComm_t (comm.cpp)
+    int nranks = 1, rank = 0, device = 0;
+    ~nori_gpu_comm() { comm_destroy(nccl); }
 };
 
 namespace {
@@ -1157,6 +1165,40 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
+namespace {
+
+// This rank's share of a whole-frame render (nori_gpu_shard_desc).
+nori_gpu_render_desc shard_of(int W, int H, uint32_t spp, const nori_gpu_render_desc &whole, int mode, int nranks,
+                              int rank, std::vector<uint32_t> &blocks) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw NoriException(NORI_ERR_INVALID, "shard: rank out of range");
+    if (mode != NORI_SHARD_PASSES && mode != NORI_SHARD_BLOCKS) throw NoriException(NORI_ERR_INVALID, "shard: unknown mode");
+    nori_gpu_render_desc out = whole;
+    const uint32_t P = whole.pass_count ? whole.pass_count : spp;
+    blocks.clear();
+    if (mode == NORI_SHARD_PASSES) {
+        const uint64_t a = (uint64_t)P * rank / nranks, b = (uint64_t)P * (rank + 1) / nranks;
+        out.pass_begin = whole.pass_begin + (uint32_t)a;
+        out.pass_count = (uint32_t)(b - a);
+        if (whole.num_blocks) blocks.assign(whole.block_ids, whole.block_ids + whole.num_blocks);
+    } else {
+        const uint32_t nb = (uint32_t)(std::ceil(W / (float)NORI_BLOCK_SIZE) * std::ceil(H / (float)NORI_BLOCK_SIZE));
+        std::vector<char> want(nb, whole.num_blocks ? 0 : 1);
+        for (uint32_t i = 0; i < whole.num_blocks; ++i) {
+            if (whole.block_ids[i] >= nb) throw NoriException(NORI_ERR_INVALID, "block id out of range");
+            want[whole.block_ids[i]] = 1;
+        }
+        uint32_t k = 0;  // round-robin over the spiral order (block.cpp:140-188)
+        for (uint32_t b : spiral_blocks(W, H))
+            if (want[b] && (k++ % (uint32_t)nranks) == (uint32_t)rank) blocks.push_back(b);
+        out.pass_count = blocks.empty() ? 0 : P;  // no block of this rank: an empty share
+    }
+    out.num_blocks = (uint32_t)blocks.size();
+    out.block_ids = blocks.empty() ? nullptr : blocks.data();
+    return out;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char *nori_gpu_last_error(void) { return g_last_error.c_str(); }
@@ -1261,6 +1303,7 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         HIP_TRY(hipSetDevice(device));
         std::unique_ptr<nori_gpu_ctx> c(new nori_gpu_ctx);
         c->device = device;
+        c->spp = d->sample_count ? d->sample_count : 1;
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         for (int h = 1; h < kMaxParts; ++h) {
@@ -1307,6 +1350,78 @@ int nori_gpu_cancel(nori_gpu_ctx *c) {
     return NORI_OK;
 }
 float nori_gpu_progress(const nori_gpu_ctx *c) { return c ? c->progress.load() : 0.0f; }
+
+int nori_gpu_comm_id(unsigned char *id) {
+    return guarded([&] {
+        if (!id) return fail(NORI_ERR_INVALID, "null argument");
+        comm_unique_id(id);
+        return (int)NORI_OK;
+    });
+}
+int nori_gpu_comm_create(const unsigned char *id, int nranks, int rank, int device, nori_gpu_comm **out) {
+    return guarded([&] {
+        if (!id || !out) return fail(NORI_ERR_INVALID, "null argument");
+        std::unique_ptr<nori_gpu_comm> c(new nori_gpu_comm);
+        c->nccl = comm_create(id, nranks, rank, device);
+        c->nranks = nranks;
+        c->rank = rank;
+        c->device = device;
+        *out = c.release();
+        return (int)NORI_OK;
+    });
+}
+int nori_gpu_comm_rank(const nori_gpu_comm *c, int *nranks, int *rank) {
+    if (!c || !nranks || !rank) return fail(NORI_ERR_INVALID, "null argument");
+    *nranks = c->nranks;
+    *rank = c->rank;
+    return NORI_OK;
+}
+void nori_gpu_comm_destroy(nori_gpu_comm *c) { delete c; }
+const char *nori_gpu_comm_library(void) { return comm_library_path(); }
+
+int nori_gpu_shard_desc(const nori_scene_desc *d, const nori_gpu_render_desc *rd, int mode, int nranks, int rank,
+                        nori_gpu_render_desc *out, uint32_t *block_buf) {
+    return guarded([&] {
+        if (!d || !rd || !out || (rd->num_blocks && !rd->block_ids)) return fail(NORI_ERR_INVALID, "null argument");
+        std::vector<uint32_t> blocks;
+        nori_gpu_render_desc s =
+            shard_of(d->camera.width, d->camera.height, d->sample_count, *rd, mode, nranks, rank, blocks);
+        if (!blocks.empty()) {
+            if (!block_buf) return fail(NORI_ERR_INVALID, "block_buf is null");
+            std::memcpy(block_buf, blocks.data(), 4 * blocks.size());
+            s.block_ids = block_buf;
+        } else {
+            s.block_ids = nullptr;
+        }
+        *out = s;
+        return (int)NORI_OK;
+    });
+}
+
+int nori_gpu_render_sharded(nori_gpu_ctx *c, nori_gpu_comm *comm, const nori_gpu_render_desc *rd, int mode, int root,
+                            float *film, nori_gpu_stats *stats) {
+    return guarded([&] {
+        if (!c || !comm || !rd || !film) return fail(NORI_ERR_INVALID, "null argument");
+        if (rd->num_blocks && !rd->block_ids) return fail(NORI_ERR_INVALID, "block_ids is null");
+        if (root >= comm->nranks) return fail(NORI_ERR_INVALID, "root out of range");
+        if (comm->device != c->device) return fail(NORI_ERR_INVALID, "communicator and context on different devices");
+        HIP_TRY(hipSetDevice(c->device));
+        std::vector<uint32_t> blocks;
+        nori_gpu_render_desc s = shard_of(c->S.W, c->S.H, c->spp, *rd, mode, comm->nranks, comm->rank, blocks);
+        s.output_on_device = 1;
+        const size_t n = 4 * (size_t)(c->S.W + 2 * c->S.border) * (size_t)(c->S.H + 2 * c->S.border);
+        HIP_TRY(hipMemsetAsync(film, 0, n * sizeof(float), c->stream));
+        int rc = NORI_OK;
+        if (s.pass_count)
+            rc = render(*c, s, film, stats);
+        else if (stats)
+            std::memset(stats, 0, sizeof(*stats));
+        if (rc != NORI_OK) return rc;  // (a failed rank leaves the others waiting in the sum: as any collective)
+        comm_sum(comm->nccl, film, n, root, c->stream);
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return (int)NORI_OK;
+    });
+}
 void nori_gpu_destroy(nori_gpu_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);

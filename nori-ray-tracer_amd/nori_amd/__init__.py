@@ -248,17 +248,7 @@ class GpuRenderer:
         address (device mode) that the per-pixel sample statistics are added
         into (see film_variance).
         """
-        rd = _abi.RenderDesc()
-        rd.pass_begin = int(pass_begin)
-        rd.pass_count = int(self.scene.spp if passes is None else passes)
-        ids = None
-        if blocks is not None:
-            ids = np.ascontiguousarray(np.asarray(blocks, dtype=np.uint32))
-            rd.num_blocks = ids.size
-            rd.block_ids = ids.ctypes.data_as(C.POINTER(C.c_uint32))
-        rd.seed = int(seed)
-        rd.path_pool = int(path_pool)
-        rd.timing = int(bool(timing))
+        rd, ids = self._desc(passes, pass_begin, blocks, seed, path_pool, timing)
         if variance is not None:
             if device_ptr is not None:
                 rd.variance_out = int(variance)
@@ -278,6 +268,31 @@ class GpuRenderer:
         check(lib().nori_gpu_render(self._h, C.byref(rd), out.ctypes.data_as(C.c_void_p), C.byref(st)))
         self.last_stats = st.as_dict()
         return out
+
+    def _desc(self, passes, pass_begin, blocks, seed, path_pool, timing):
+        rd = _abi.RenderDesc()
+        rd.pass_begin = int(pass_begin)
+        rd.pass_count = int(self.scene.spp if passes is None else passes)
+        ids = None
+        if blocks is not None:
+            ids = np.ascontiguousarray(np.asarray(blocks, dtype=np.uint32))
+            rd.num_blocks = ids.size
+            rd.block_ids = ids.ctypes.data_as(C.POINTER(C.c_uint32))
+        rd.seed = int(seed)
+        rd.path_pool = int(path_pool)
+        rd.timing = int(bool(timing))
+        return rd, ids
+
+    def render_sharded(self, comm, device_ptr, passes=None, pass_begin=0, blocks=None, mode="passes", root=0,
+                       seed=0, path_pool=0, timing=False):
+        """This rank's share of the frame into the device film at `device_ptr`
+        (zeroed first), then the RCCL sum of every rank's film into root's
+        (root=-1: into every rank's) -- nori_gpu_render_sharded."""
+        rd, ids = self._desc(passes, pass_begin, blocks, seed, path_pool, timing)
+        st = _abi.Stats()
+        check(lib().nori_gpu_render_sharded(self._h, comm.handle, C.byref(rd), _abi.SHARD_MODES[mode], int(root),
+                                            C.c_void_p(int(device_ptr)), C.byref(st)))
+        self.last_stats = st.as_dict()
 
     def trace(self, rays, any_hit=False):
         """Scene::rayIntersect on a batch: rays (n, 8) = o.xyz, mint, d.xyz, maxt."""

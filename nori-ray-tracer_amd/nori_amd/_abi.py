@@ -131,7 +131,20 @@ SIGNATURES = {
     "nori_gpu_cancel": (C.c_int, [C.c_void_p]),
     "nori_gpu_progress": (C.c_float, [C.c_void_p]),
     "nori_gpu_destroy": (None, [C.c_void_p]),
+    "nori_gpu_comm_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
+    "nori_gpu_comm_create": (C.c_int, [C.POINTER(C.c_ubyte), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "nori_gpu_comm_rank": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "nori_gpu_comm_destroy": (None, [C.c_void_p]),
+    "nori_gpu_comm_library": (C.c_char_p, []),
+    "nori_gpu_shard_desc": (C.c_int, [C.POINTER(SceneDesc), C.POINTER(RenderDesc), C.c_int, C.c_int, C.c_int,
+                                      C.POINTER(RenderDesc), C.POINTER(C.c_uint32)]),
+    "nori_gpu_render_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(RenderDesc), C.c_int, C.c_int,
+                                          C.c_void_p, C.POINTER(Stats)]),
 }
+
+COMM_ID_BYTES = 128
+SHARD_PASSES, SHARD_BLOCKS = 0, 1
+SHARD_MODES = {"passes": SHARD_PASSES, "blocks": SHARD_BLOCKS}
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # NORI_GPU_LIB: another in-tree build of the library (tuning variants under lib/)
@@ -140,12 +153,38 @@ LIB_PATH = os.environ.get("NORI_GPU_LIB") or os.path.join(PKG_DIR, "lib", "libno
 _lib = None
 
 
+def _one_hip_runtime():
+    """Make libnori_gpu share the process's single HIP runtime with PyTorch.
+
+    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 (torch/lib,
+    found through its $ORIGIN rpath by file name), while libnori_gpu needs
+    them by SONAME (libamdhip64.so.7), which the loader resolves to /opt/rocm.
+    Loaded in that order a process maps TWO HIP runtimes, and whichever
+    initialises second sees no device ("No HIP GPUs are available").  So when
+    torch is installed, its runtime is mapped first (RTLD_GLOBAL): libnori_gpu's
+    SONAME dependency then binds to it, and a later `import torch` finds the
+    same files already mapped.  NORI_HIP_RUNTIME=system keeps /opt/rocm's."""
+    if os.environ.get("NORI_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")  # locates torch without importing it
+    if spec is None or not spec.origin:
+        return
+    tlib = os.path.join(os.path.dirname(spec.origin), "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        path = os.path.join(tlib, name)
+        if os.path.exists(path):
+            C.CDLL(path, mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+
+
 def lib():
     """Load libnori_gpu.so from the package tree; fail loudly if it is missing."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libnori_gpu.so not built: {LIB_PATH} (run __graft_entry__.build())")
+        _one_hip_runtime()
         l = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(l, name)

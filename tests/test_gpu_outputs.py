@@ -45,7 +45,7 @@ def test_variance_statistics_match_oracle(built, xml, size):
     assert np.isfinite(var).all() and (var >= 0).all() and var.max() > 0
 
 
-# device-memory statistics (torch tensors): tests/test_gpu_torch.py, check "device_variance"
+# device-memory statistics (torch tensors): tests/test_gpu_torch.py::test_variance_statistics_device_buffers
 
 
 def test_cli_writes_exr_variance_png(built, tmp_path):

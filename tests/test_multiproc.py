@@ -1,5 +1,8 @@
-"""Multi-process sharding on CPU (gloo, world size 2): the same logic bench.py
-runs over RCCL, with the oracle as the per-rank renderer."""
+"""Multi-process sharding on CPU (gloo): the split bench.py --gpus N and
+nori_gpu_render_sharded use (nori_gpu_shard_desc, the library's C code),
+with the oracle as each rank's renderer and a gloo all_reduce in place of the
+RCCL film sum.  The summed film must equal the single-process render of the
+whole frame (same WAVE streams; only the float summation order differs)."""
 import os
 import socket
 
@@ -12,6 +15,7 @@ import torch.multiprocessing as mp
 from conftest import ROOT, scene_path
 
 SCENE = scene_path("pa4", "cbox", "cbox_path_mis.xml")
+W, H, SPP = 80, 48, 5  # 3x2 blocks (ragged last column), 5 passes: uneven splits
 
 
 def _free_port():
@@ -34,29 +38,52 @@ def _worker(rank, world, port, mode, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    scene = nori_amd.load_scene(SCENE, 64, 48, 2)
-    o = pyoracle.OracleScene(scene)
-    if mode == "passes":
-        pb, pc = nd.pass_range(rank, 2)
-        film = o.render(passes=pc, pass_begin=pb, rng="wave", threads=2)
-    else:
-        film = o.render(passes=4, rng="wave", blocks=nd.block_subset(rank, world, scene.num_blocks()), threads=2)
+    scene = nori_amd.load_scene(SCENE, W, H, SPP)
+    pb, pc, blocks = nd.shard(scene, rank, world, mode)
+    film = np.zeros(scene.film_shape(), np.float32)
+    if pc:
+        pyoracle.OracleScene(scene).render(passes=pc, pass_begin=pb, rng="wave", blocks=blocks, threads=2, out=film)
     t = torch.from_numpy(film)
-    nd.reduce_film(t, dist)
+    dist.all_reduce(t)  # the film sum nori_gpu_render_sharded does over RCCL
     if rank == 0:
         np.save(out_path, t.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("mode", ["passes", "blocks"])
-def test_two_rank_sharding_matches_single_process(built, tmp_path, mode):
+def test_sharded_frame_matches_single_process(built, tmp_path, mode, world):
     import nori_amd
     import pyoracle
 
     out = str(tmp_path / "film.npy")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True,
+                       start_method="spawn")
     got = np.load(out)
-    scene = nori_amd.load_scene(SCENE, 64, 48, 2)
-    ref = pyoracle.OracleScene(scene).render(passes=4, rng="wave")
+    scene = nori_amd.load_scene(SCENE, W, H, SPP)
+    ref = pyoracle.OracleScene(scene).render(rng="wave")
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_shard_partitions_the_frame(built):
+    """Every (pass, block) of the frame is in exactly one rank's share, for
+    more ranks than passes or blocks too (empty shares)."""
+    import nori_amd
+    from nori_amd import distributed as nd
+
+    scene = nori_amd.load_scene(SCENE, W, H, SPP)
+    nb = scene.num_blocks()
+    for mode in ("passes", "blocks"):
+        for world in (1, 2, 3, 4, 7, 9):
+            seen = np.zeros((SPP, nb), np.int32)
+            for r in range(world):
+                pb, pc, blocks = nd.shard(scene, r, world, mode)
+                for b in (range(nb) if blocks is None else blocks):
+                    seen[pb:pb + pc, b] += 1
+            assert (seen == 1).all(), (mode, world)
+    # restricted frame: a block subset split again over the ranks
+    sub = [0, 2, 5]
+    got = sorted(b for r in range(2) for b in nd.shard(scene, r, 2, "blocks", blocks=sub)[2])
+    assert got == sub
+    assert nd.shard(scene, 1, 2, "passes", passes=4, pass_begin=10)[:2] == (12, 2)
