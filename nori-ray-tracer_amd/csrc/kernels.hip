@@ -929,12 +929,22 @@ ND float env_pdf(const DevScene &S, const DevEmitter &e, V3 wi) {
     const int i = clampi((int)uv.x, 0, e.R - 1), j = clampi((int)uv.y, 0, e.C - 1);
     return S.env[e.pmarg_off + i] * S.env[e.pdf_off + (size_t)i * e.C + j];
 }
-// sample1D (envmap.cpp:112-122); an all-zero row takes its last interval
+// sample1D (envmap.cpp:112-122): the reference scans for the first i with
+// P[i] <= s < P[i+1] (the oracle keeps that scan).  P[0..cols-1] is
+// nondecreasing (P[0] = 0 plus non-negative pf terms; only the final
+// P[cols] = 1 of the literal precompute1D can drop below P[cols-1]), so the
+// first such i below cols-1 is upper_bound(P[0..cols-1], s) - 1, and every
+// other case -- s >= P[cols-1], or no interval at all (all-zero rows, NaN s)
+// -- ends at cols-1 in the scan too.  Binary search: O(log cols) loads
+// instead of up to cols dependent pairs per environment sample.
 ND void env_sample1D(const float *pf, const float *P, int cols, float s, float &x, float &prob) {
-    int i;
-    for (i = 0; i < cols; i++)
-        if (P[i] <= s && s < P[i + 1]) break;
-    if (i >= cols) i = cols - 1;
+    int lo = 0, hi = cols;  // first j in [0, cols) with P[j] > s, or cols
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (P[mid] <= s) lo = mid + 1;
+        else hi = mid;
+    }
+    const int i = (lo == 0 || lo >= cols) ? cols - 1 : lo - 1;
     const float t = (P[i + 1] - s) / (P[i + 1] - P[i]);
     x = (1 - t) * (float)i + t * (float)(i + 1);
     prob = pf[i];
@@ -1594,8 +1604,10 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
             // the last segment to run dry tells the host (system-scope store to
             // host-mapped memory) -- no per-iteration readback is needed
             uint32_t n = atomicAdd(&C->exhausted, 1u) + 1u;
-            // progress hint: plain system-scope store (no PCIe atomics needed)
-            __hip_atomic_store(wd.done_flag + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // progress hint: plain system-scope store (no PCIe atomics needed),
+            // every 64th exhausted segment only (a store to host memory per
+            // segment slowed the last iterations measurably)
+            if ((n & 63u) == 0u) __hip_atomic_store(wd.done_flag + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (n == wd.G) __hip_atomic_store(wd.done_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }

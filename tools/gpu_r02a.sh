@@ -5,7 +5,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 echo "affinity $(python3 -c 'import os;print(len(os.sched_getaffinity(0)))') cpu.max $(cat /sys/fs/cgroup/cpu.max 2>/dev/null) nproc $(nproc)"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest ${PYTEST_SEL:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 b() { # name, args...
@@ -14,7 +14,6 @@ b() { # name, args...
   r=$?; echo "bench $n rc=$r"; tail -c 600 gpurun_out/bench_$n.log | tail -2; return $r
 }
 b c2 --steps 10 --warmup 3 && \
-NORI_HIP_RUNTIME=system b c2sys --steps 10 --warmup 3 --no-cpu-baseline --no-parity && \
 b c2spp64 --spp 64 --steps 10 --warmup 3 --no-cpu-baseline --no-parity && \
 b c2spp128 --spp 128 --steps 10 --warmup 3 --no-cpu-baseline --no-parity && \
 b c5 --config c5 --steps 3 --warmup 1 --cpu-seconds 8 && \
