@@ -79,6 +79,9 @@ struct DevScene {
     float filter_radius, lookup;
     int32_t border;
     int32_t integrator;
+    // 1: next-event estimation at a mirror/dielectric vertex only draws its
+    // three random numbers (deviation D10; no environment-map emitter)
+    int32_t skip_discrete_nee;
     // homogeneous medium (medium.cpp)
     int32_t has_medium;
     float mbox_min[3], mbox_max[3];
@@ -193,8 +196,7 @@ struct Counters {
     uint32_t exhausted;            // segments whose work stream is used up
     uint32_t pad0[31];
     unsigned long long invalid;    // dropped samples (splat)
-    unsigned long long prof[8];    // profiling builds only (NORI_PROF_FINISH): finisher phase clocks
-    unsigned long long pad1[7];
+    unsigned long long prof[15];   // profiling builds only (NORI_PROF_SHADE / NORI_PROF_FINISH): phase clocks
     uint32_t finish_paths;         // paths completed by the tail finisher
     uint32_t finish_max_rays;      // most rays traced by one finisher path
     uint32_t pad2[30];

@@ -84,6 +84,9 @@ NHD void pcg_seed(Pcg &r, uint64_t initstate, uint64_t initseq) {
     r.state += initstate;
     pcg_next(r);
 }
+NHD void pcg_skip(Pcg &r, int n) {  // n draws whose values are not needed
+    for (int i = 0; i < n; ++i) r.state = r.state * kPcgMult + r.inc;
+}
 NHD float pcg_float(Pcg &r) {
     uint32_t u = (pcg_next(r) >> 9) | 0x3f800000u;
     float f;

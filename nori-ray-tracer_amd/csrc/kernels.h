@@ -21,9 +21,13 @@ constexpr int stack_lds_entries(int stack) { return NORI_STACK_KEYS ? stack / 2 
 constexpr int kTraceGroup = NORI_TRACE_GROUP;  // segments per extend/shadow work-group
 constexpr int kSplatBlock = 256;
 #ifndef NORI_SCAN_RAYS
-#define NORI_SCAN_RAYS 1
+#define NORI_SCAN_RAYS 2
 #endif
-constexpr int kScanRays = NORI_SCAN_RAYS;  // rays per thread of the scan-mode trace kernels
+constexpr int kScanRays = NORI_SCAN_RAYS;  // rays per thread of the scan-mode extension kernel
+#ifndef NORI_SCAN_RAYS_SHADOW
+#define NORI_SCAN_RAYS_SHADOW 1
+#endif
+constexpr int kScanRaysShadow = NORI_SCAN_RAYS_SHADOW;  // ... and of the scan-mode shadow kernel
 #ifndef NORI_SHADE_LDS_MAX
 #define NORI_SHADE_LDS_MAX 16384
 #endif

@@ -478,6 +478,29 @@ ND void extend_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt,
     }
 }
 
+// Unoccluded shadow ray: record += payload (the reference's `color +=`,
+// path_mis.cpp:48-60).  A record belongs to one path, which has at most one
+// shadow ray per launch, so a plain read-modify-write is race free; it runs
+// after the traversal, for unoccluded rays only (reading every ray's record
+// before the scan fetched 2.3x the algorithmic bytes).  NORI_SHADOW_ATOMIC=1:
+// three returnless float atomics instead (same IEEE sums; measured 1.8x
+// slower on cbox: every atomic writes its line through).
+#ifndef NORI_SHADOW_ATOMIC
+#define NORI_SHADOW_ATOMIC 0
+#endif
+ND void shadow_add(float4 *rec, const float4 &c) {
+#if NORI_SHADOW_ATOMIC
+    float *r = reinterpret_cast<float *>(rec + __float_as_uint(c.w));
+    atomicAdd(r + 0, c.x);
+    atomicAdd(r + 1, c.y);
+    atomicAdd(r + 2, c.z);
+#else
+    const uint32_t w = __float_as_uint(c.w);
+    const float4 L = rec[w];
+    rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
+#endif
+}
+
 // Shadow rays: any hit; unoccluded -> record += payload.
 template <int STACK>
 ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
@@ -494,12 +517,7 @@ ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *sh
         r.maxt = b.w;
         float t, u, v;
         uint32_t p;
-        if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) {
-            float4 c = sq.payload[q];
-            uint32_t w = __float_as_uint(c.w);
-            float4 L = rec[w];
-            rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
-        }
+        if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) shadow_add(rec, sq.payload[q]);
     }
 }
 
@@ -727,12 +745,7 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(Dev
         // ---- retire finished rays
         if (active && !has_ref && !has_leaf) {
             if (ANY) {
-                if (!found) {
-                    const float4 c = J.payload[q];
-                    const uint32_t w = __float_as_uint(c.w);
-                    const float4 Lr = J.rec[w];
-                    J.rec[w] = make_float4(Lr.x + c.x, Lr.y + c.y, Lr.z + c.z, Lr.w);
-                }
+                if (!found) shadow_add(J.rec, J.payload[q]);
             } else {
                 J.hit[q] = make_float4(tb, __uint_as_float(pb), ub, vb);
             }
@@ -815,10 +828,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
     TRay r[K];
     bool live[K], valid[K];
     uint32_t q[K];
-    // unconditional loads (lanes past the end repeat entry i0); payload and
-    // record are fetched before the scan, for occluded rays too, so their
-    // latency hides behind the traversal instead of stalling the wave's end
-    float4 c[K], L[K];
+    // unconditional loads (lanes past the end repeat entry i0); the payload is
+    // fetched before the scan so its latency hides behind the traversal
+    float4 c[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t i = i0 + k * kTraceBlock;
@@ -831,16 +843,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
         r[k].mint = a.w;
         r[k].maxt = b.w;
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) L[k] = rec[__float_as_uint(c[k].w)];
     float t[K], u[K], v[K];
     uint32_t p[K];
     bool f[K];
     scan_rays<K, true>(S, r, live, t, p, u, v, f);
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        if (valid[k] && !f[k])
-            rec[__float_as_uint(c[k].w)] = make_float4(L[k].x + c[k].x, L[k].y + c[k].y, L[k].z + c[k].z, L[k].w);
+        if (valid[k] && !f[k]) shadow_add(rec, c[k]);
 }
 
 // ------------------------------------------------------------------ shading helpers
@@ -1271,6 +1280,20 @@ ND void rec_add(float4 *rec, PathState &ps, const V3 &a) {
 #endif
 }
 
+// Deviation D10: a mirror or dielectric BSDF evaluates to exactly zero, so
+// the NEE term at such a vertex, attenuation * w_ems * 0 * theta * Li, is zero
+// whenever its other factors are finite.  Then only its three random numbers
+// (emitter choice, 2D light sample) are drawn and no light is sampled: RR and
+// the BSDF sample read the same stream positions, the image is bit-identical.
+// Kept in full when the attenuation is not finite or the scene has an
+// environment map (its Li can be inf/NaN, which the reference turns into an
+// invalid sample); for area/point lights Li is finite unless the vertex
+// coincides exactly with the sampled light point.
+ND bool skip_nee(const DevScene &S, const DevBsdf &B, const V3 &beta) {
+    return S.skip_discrete_nee && (B.type == NORI_BSDF_MIRROR || B.type == NORI_BSDF_DIELECTRIC) &&
+           isfinite(beta.x) && isfinite(beta.y) && isfinite(beta.z);
+}
+
 // One iteration of VolumetricIntegrator::Li (volumetric.cpp:18-156) for the
 // current segment (ps.o, ps.d) and its closest hit h (prim ~0: none, t = inf).
 // Free flight first: a scattering event does phase-function NEE with
@@ -1327,7 +1350,9 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
         rec_add<ATOMIC>(rec, ps, Ladd);
     }
-    {
+    if (skip_nee(S, B, ps.beta)) {
+        pcg_skip(ps.rng, 3);
+    } else {
         NeeSample ne = nee_sample(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
@@ -1401,7 +1426,9 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         (void)next2D(ps.rng);
     } else
 #endif
-    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
+    if (INTEG == NORI_INTEGRATOR_PATH_MIS && skip_nee(S, B, ps.beta)) {
+        pcg_skip(ps.rng, 3);
+    } else if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
         const NeeSample ne = nee_sample(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
@@ -1663,23 +1690,33 @@ __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg,
 
 // Cooperative scan (scan-mode scenes, n <= 64 primitives): the rays of the
 // lanes in `want` are traced one after another by the whole wave, lane l
-// testing primitive l against the broadcast ray, then a wave reduction.  The
-// result is exactly that of traverse<0, ANY> for the ray: every candidate
-// passes the test against the ray's own maxt, the closest wins, and among
-// equal t the last primitive in scan order wins (the `t <= maxt` update).
-// A lone tail path then pays one primitive test per ray instead of n.
-template <bool ANY>
-ND bool coop_scan(const DevScene &S, const TRay &mine, bool want, float &t, uint32_t &p, float &u, float &v) {
+// testing primitive l against the broadcast ray.  The result is exactly that
+// of traverse<0, ANY> for the ray: every candidate passes the test against the
+// ray's own maxt, the closest wins, and among equal t the last primitive in
+// scan order wins (the `t <= maxt` update).  A lone tail path then pays one
+// primitive test per ray instead of n.
+struct CoopPrim {  // lane l's primitive, loaded once per finisher wave
+    float4 p0, p1, p2;
+    bool has, tri;
+};
+ND CoopPrim coop_load(const DevScene &S) {
+    CoopPrim c;
     const uint32_t lane = lane_id();
-    const bool has = lane < S.num_prims;
-    float4 p0 = make_float4(0, 0, 0, 0), p1 = p0, p2 = p0;
-    if (has) {
+    c.has = lane < S.num_prims;
+    c.p0 = c.p1 = c.p2 = make_float4(0, 0, 0, 0);
+    if (c.has) {
         const float4 *pp = S.prims + 3 * (size_t)lane;
-        p0 = pp[0];
-        p1 = pp[1];
-        p2 = pp[2];
+        c.p0 = pp[0];
+        c.p1 = pp[1];
+        c.p2 = pp[2];
     }
-    const bool tri = __float_as_uint(p1.w) == 0u;
+    c.tri = __float_as_uint(c.p1.w) == 0u;
+    return c;
+}
+template <bool ANY>
+ND bool coop_scan(const DevScene &S, const CoopPrim &cp, const TRay &mine, bool want, float &t, uint32_t &p, float &u,
+                  float &v) {
+    const uint32_t lane = lane_id();
     const float4 rmn = make_float4(S.root_min[0], S.root_min[1], S.root_min[2], 0.f);
     const float4 rmx = make_float4(S.root_max[0], S.root_max[1], S.root_max[2], 0.f);
     bool res = false;
@@ -1702,35 +1739,35 @@ ND bool coop_scan(const DevScene &S, const TRay &mine, bool want, float &t, uint
         const bool live = !(r.maxt < r.mint) && box_test(rmn, rmx, r, tn);
         float tl = 0, ul = 0, vl = 0;
         bool hl = false;
-        if (has) hl = tri ? tri_hit_nb(p0, p1, p2, r, tl, ul, vl) : sphere_hit_nb(p0, p1, r, tl);
-        hl = hl && live;
+        if (cp.has) hl = cp.tri ? tri_hit_nb(cp.p0, cp.p1, cp.p2, r, tl, ul, vl) : sphere_hit_nb(cp.p0, cp.p1, r, tl);
+        uint64_t hm = __ballot(hl && live);
         if (ANY) {
-            const bool any = __ballot(hl) != 0ull;
-            if ((int)lane == j) res = any;
-        } else {
-            // key: t (positive, so its bits order like the value), then the
-            // highest lane among equal t
-            uint32_t khi = hl ? __float_as_uint(tl + 0.0f) : 0xFFFFFFFFu, klo = hl ? 63u - lane : 0xFFFFFFFFu;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                uint32_t ohi = (uint32_t)__shfl_xor((int)khi, o), olo = (uint32_t)__shfl_xor((int)klo, o);
-                bool take = ohi < khi || (ohi == khi && olo < klo);
-                khi = take ? ohi : khi;
-                klo = take ? olo : klo;
+            if ((int)lane == j) res = hm != 0ull;
+            continue;
+        }
+        if (!hm) continue;
+        // closest hit over the (few) hitting lanes, walked in lane order with
+        // `<=` so that the last primitive among equal t wins; t > 0, so its
+        // bits order like the value and the comparison stays scalar
+        uint32_t best = 0xFFFFFFFFu;
+        int w = 0;
+        do {
+            const int l = __builtin_ctzll(hm);
+            hm &= hm - 1;
+            const uint32_t tb = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(tl + 0.0f), l);
+            if (tb <= best) {
+                best = tb;
+                w = l;
             }
-            const uint32_t lo = __builtin_amdgcn_readfirstlane(klo);
-            if (lo != 0xFFFFFFFFu) {
-                const int w = 63 - (int)lo;
-                const float tw = bcast(tl, w), uw = bcast(tri ? ul : 0.0f, w), vw = bcast(tri ? vl : 0.0f, w);
-                const uint32_t pw = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(p0.w), w);
-                if ((int)lane == j) {
-                    res = true;
-                    t = tw;
-                    p = pw;
-                    u = uw;
-                    v = vw;
-                }
-            }
+        } while (hm);
+        const float tw = __uint_as_float(best), uw = bcast(cp.tri ? ul : 0.0f, w), vw = bcast(cp.tri ? vl : 0.0f, w);
+        const uint32_t pw = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(cp.p0.w), w);
+        if ((int)lane == j) {
+            res = true;
+            t = tw;
+            p = pw;
+            u = uw;
+            v = vw;
         }
     }
     return res;
@@ -1738,7 +1775,10 @@ ND bool coop_scan(const DevScene &S, const TRay &mine, bool want, float &t, uint
 
 // At most this many tracing lanes use the cooperative scan (each costs one
 // primitive test per lane and a reduction; the per-lane scan costs n tests).
-constexpr int kCoopMax = 4;
+#ifndef NORI_COOP_MAX
+#define NORI_COOP_MAX 4
+#endif
+constexpr int kCoopMax = NORI_COOP_MAX;
 
 // Runs every path still queued to completion, one thread per path: the
 // Russian-roulette tail (a glass-sphere path survives with q = 0.99 per
@@ -1815,25 +1855,35 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         ps.L = ld3(rec[ps.work]);
     }
     uint32_t rays = 0;
+    const bool coop = STACK == 0 && S.num_prims <= 64;
+    CoopPrim cp;
+    if (coop) cp = coop_load(S);
     auto trace = [&](const TRay &r, bool want, bool any_hit, float &t, uint32_t &p, float &u, float &v) -> bool {
-        if (STACK == 0 && S.num_prims <= 64 && __popcll(__ballot(want)) <= kCoopMax)
-            return any_hit ? coop_scan<true>(S, r, want, t, p, u, v) : coop_scan<false>(S, r, want, t, p, u, v);
+        if (coop && __popcll(__ballot(want)) <= kCoopMax)
+            return any_hit ? coop_scan<true>(S, cp, r, want, t, p, u, v) : coop_scan<false>(S, cp, r, want, t, p, u, v);
         if (!want) return false;
         return any_hit ? traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)
                        : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
     };
 #ifdef NORI_PROF_FINISH  // profiling build: clocks of the loop's phases, summed over waves
-    uint64_t pt[4] = {0, 0, 0, 0}, pc = __builtin_amdgcn_s_memtime();
+    uint64_t pt[4] = {0, 0, 0, 0}, pc = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime(), wit = 0;
+    uint64_t p1[4] = {0, 0, 0, 0}, n1 = 0;  // iterations with a single active lane
+    bool solo = false;
 #define NORI_PHASE(i)                                        \
     {                                                        \
         const uint64_t now = __builtin_amdgcn_s_memtime();   \
         pt[i] += now - pc;                                   \
+        if (solo) p1[i] += now - pc;                         \
         pc = now;                                            \
     }
 #else
 #define NORI_PHASE(i)
 #endif
     while (__ballot(active)) {
+#ifdef NORI_PROF_FINISH
+        solo = __popcll(__ballot(active)) == 1;
+        n1 += solo ? 1 : 0;
+#endif
         ShadowOut so;
         so.emit = false;
         bool alive = false;
@@ -1872,11 +1922,18 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         NORI_PHASE(3)
 #ifdef NORI_PROF_FINISH
         if (lane_id() == 0) atomicAdd(&C->prof[4], 1ull);
+        ++wit;
 #endif
     }
 #ifdef NORI_PROF_FINISH
-    if (lane_id() == 0)
+    if (lane_id() == 0) {
         for (int i = 0; i < 4; ++i) atomicAdd(&C->prof[i], (unsigned long long)pt[i]);
+        for (int i = 0; i < 4; ++i) atomicAdd(&C->prof[8 + i], (unsigned long long)p1[i]);
+        atomicAdd(&C->prof[12], (unsigned long long)n1);
+        // the longest-running wave: its span in 100 MHz ticks (high bits) and loop iterations
+        const uint64_t span = __builtin_amdgcn_s_memrealtime() - rt0;
+        atomicMax(&C->prof[5], (unsigned long long)((span << 20) | (wit & 0xFFFFFu)));
+    }
 #endif
 #undef NORI_PHASE
 }
@@ -2403,9 +2460,9 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
-    if (stack == 0 && kScanRays > 1) {
-        dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
-        hipLaunchKernelGGL(k_shadow_scan<kScanRays>, gk, b, 0, st, S, sq, shcnt, rec, G);
+    if (stack == 0 && kScanRaysShadow > 1) {
+        dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRaysShadow));
+        hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, b, 0, st, S, sq, shcnt, rec, G);
         return hipGetLastError();
     }
     switch (stack) {

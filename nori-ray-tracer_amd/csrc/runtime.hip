@@ -580,6 +580,12 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.border = film_border(cam);
     if (S.border > 4) throw NoriException(NORI_ERR_UNSUPPORTED, "filter radius above 4.5 pixels");
     S.integrator = d.integrator;
+    {  // deviation D10 (kernels.hip skip_nee); NORI_DISCRETE_NEE=1 keeps the full NEE everywhere
+        bool env = false;
+        for (uint32_t i = 0; i < d.num_emitters; ++i) env = env || d.emitters[i].type == NORI_EMITTER_ENVMAP;
+        const char *e = std::getenv("NORI_DISCRETE_NEE");
+        S.skip_discrete_nee = !env && !(e && e[0] == '1');
+    }
     S.has_medium = d.medium.present;
     if (S.has_medium) {  // medium.cpp:10-20
         const nori_medium_desc &m = d.medium;
@@ -1111,9 +1117,15 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                              (double)hc.prof[2] / hc.prof[6], (double)hc.prof[3] / hc.prof[6],
                              (double)hc.prof[4] / hc.prof[6], (double)hc.prof[5] / hc.prof[6], hc.prof[6]);
             else if (hc.prof[4])  // NORI_PROF_FINISH builds
-                std::fprintf(stderr, "[nori] finisher clocks per wave-iteration: shade %.0f shadow %.0f splat %.0f extend %.0f (%llu)\n",
+                std::fprintf(stderr, "[nori] finisher clocks per wave-iteration: shade %.0f shadow %.0f splat %.0f extend %.0f (%llu); "
+                             "longest wave %.3f ms over %llu iterations\n",
                              (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4],
-                             (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
+                             (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4],
+                             (double)(hc.prof[5] >> 20) * 1e-5, hc.prof[5] & 0xFFFFFull);
+            if (hc.prof[12])
+                std::fprintf(stderr, "[nori] finisher single-lane iterations: shade %.0f shadow %.0f splat %.0f extend %.0f clocks (%llu)\n",
+                             (double)hc.prof[8] / hc.prof[12], (double)hc.prof[9] / hc.prof[12],
+                             (double)hc.prof[10] / hc.prof[12], (double)hc.prof[11] / hc.prof[12], hc.prof[12]);
         }
         done_before += wd.total;
     }

@@ -5,7 +5,7 @@
 # usage: VARIANT_ENVS="..." tools/gpu_variants.sh [bench args...]
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-summ() { grep '^{' "$1" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(' ', round(d['value'],1), d['wavefront_iterations'], {k: round(v,2) for k,v in d['kernel_ms'].items()})"; }
+summ() { grep '^{' "$1" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(' ', round(d['value'],1), d['wavefront_iterations'], {k: round(v,2) for k,v in (d.get('kernel_ms_isolated') or {}).items()})"; }
 for lib in nori-ray-tracer_amd/lib/libnori_gpu.so nori-ray-tracer_amd/lib/var/*.so; do
   [ -f "$lib" ] || continue
   n=$(basename $lib .so)
