@@ -22,6 +22,7 @@
  *   nori_film_develop     <- ImageBlock::toBitmap         src/block.cpp:76-82
  *   nori_write_exr        <- Bitmap::save                 src/bitmap.cpp:82-107
  *   nori_read_exr         <- Bitmap::Bitmap(filename)     src/bitmap.cpp:23-80
+ *   nori_read_image       <- stbi_load in ImageTexture / NormalMap  src/imagetexture.cpp:69-85
  *   nori_write_png        <- Bitmap::saveToLDR            src/bitmap.cpp:122-139
  *   nori_film_variance    <- renderScene's variance image src/render.cpp:164-169,190-245
  *   nori_denoise          <- denoiser/denoiser.py:53-66 (NL-means)
@@ -48,7 +49,7 @@
 extern "C" {
 #endif
 
-#define NORI_GPU_ABI_VERSION 4
+#define NORI_GPU_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 #define NORI_OK               0
@@ -77,8 +78,11 @@ enum {
 };
 enum {
     NORI_TEXTURE_CONSTANT = 0,     /* "constant_color"     src/consttexture.cpp */
-    NORI_TEXTURE_CHECKERBOARD = 1  /* "checkerboard_color" src/checkerboard.cpp */
+    NORI_TEXTURE_CHECKERBOARD = 1, /* "checkerboard_color" src/checkerboard.cpp */
+    NORI_TEXTURE_IMAGE = 2         /* "ImageTexture"       src/imagetexture.cpp */
 };
+/* ImageWrap (include/nori/common.h:273-283): "repeat" | "clamp" */
+enum { NORI_WRAP_REPEAT = 0, NORI_WRAP_CLAMP = 1 };
 enum {
     NORI_CAMERA_PERSPECTIVE = 0,   /* "perspective"    src/perspective.cpp    */
     NORI_CAMERA_THINLENS = 1,      /* "thinlens"       src/thinlens.cpp       */
@@ -127,6 +131,9 @@ typedef struct nori_shape_desc {
     float radius;                 /* sphere                                    */
     int32_t bsdf;                 /* index into bsdfs[]                         */
     int32_t emitter;              /* index into emitters[] or -1               */
+    int32_t normal_map;           /* "NormalMap" texture named "normal": index
+                                     into images[] or -1 (shape.cpp:59-67;
+                                     applied to meshes with normals, mesh.cpp:147-155) */
 } nori_shape_desc;
 
 typedef struct nori_bsdf_desc {
@@ -141,7 +148,16 @@ typedef struct nori_bsdf_desc {
                                      checkerboard uses albedo as value1        */
     float tex_value2[3];          /* checkerboard value2                        */
     float tex_delta[2], tex_scale[2]; /* checkerboard delta (def 0), scale (def 1) */
+    int32_t albedo_image;         /* NORI_TEXTURE_IMAGE: index into images[], else -1 */
 } nori_bsdf_desc;
+
+/* An 8-bit RGB image of an ImageTexture or NormalMap, as stbi_load(path, ..,
+ * STBI_rgb) returns it: width x height x 3 bytes, top row first. */
+typedef struct nori_image_desc {
+    int32_t width, height;
+    int32_t wrap;                 /* NORI_WRAP_*                                */
+    const uint8_t *rgb;
+} nori_image_desc;
 
 typedef struct nori_emitter_desc {
     int32_t type;                 /* NORI_EMITTER_*                            */
@@ -201,6 +217,8 @@ typedef struct nori_scene_desc {
     uint32_t photon_count;        /* photonmapper "photonCount" (photons stored) */
     float photon_radius;          /* photonmapper "photonRadius" (0 in the XML:
                                      scene box diagonal / 500, photonmapper.cpp:55-56) */
+    uint32_t num_images;          /* image textures and normal maps            */
+    const nori_image_desc *images;
 } nori_scene_desc;
 
 /* ---- host-side scene loading (the plugin boundary) ----------------------- */
@@ -246,6 +264,11 @@ int nori_denoise(int device, const float *rgb, const float *variance, int width,
  * FLOAT) <- Bitmap::Bitmap (bitmap.cpp:23-80).  Call with rgb = NULL to get
  * the size, then with a buffer of 3*width*height floats (row-major). */
 int nori_read_exr(const char *path, int *width, int *height, float *rgb);
+/* Decode an image texture file as the reference's stbi_load(path, .., STBI_rgb)
+ * does (stb_image v1.39: baseline JPEG, 8-bit PNG) <- ImageTexture / NormalMap
+ * constructors (imagetexture.cpp:69-85, normalmap.cpp:69-85).  Call with
+ * rgb = NULL to get the size, then with 3*width*height bytes (top row first). */
+int nori_read_image(const char *path, int *width, int *height, uint8_t *rgb);
 
 /* Host-side BVH build of the scene exactly as nori_gpu_create builds it (no
  * device needed) <- BVH::build + BVH::statistics (bvh.cpp:329-402): node count

@@ -27,7 +27,8 @@ struct DevShape {
     uint32_t prim_offset, prim_count, cdf_offset, has_uvs;
     float center[3], radius;
     float area_norm;     // DiscretePDF::getNormalization (mesh) or sphere pdf
-    float pad2[3];
+    int32_t nm_w, nm_h, nm_wrap;  // NormalMap (meshes with normals, mesh.cpp:147-155)
+    const uint32_t *nmap;         // RGBX8 texels in global memory, or null
 };
 
 // 128 B.  Area: radiance.  Envmap (envmap.cpp): R x C texels (R = Bitmap rows,

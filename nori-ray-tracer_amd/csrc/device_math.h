@@ -229,9 +229,35 @@ struct DevBsdf {
     float kd[3];
     float base[3];
     float metallic, specular, roughness, sheen, sheen_tint, spec_tint, d_alpha;
-    int32_t tex;  // diffuse albedo: NORI_TEXTURE_CONSTANT (albedo) or _CHECKERBOARD (albedo = value1)
+    int32_t tex;  // diffuse albedo: NORI_TEXTURE_CONSTANT (albedo), _CHECKERBOARD (albedo = value1) or _IMAGE
     float tex_v2[3], tex_delta[2], tex_scale[2];
+    int32_t img_w, img_h, img_wrap;  // NORI_TEXTURE_IMAGE: RGBX8 texels in global memory
+    const uint32_t *img;
 };
+
+// ImageTexture::getData / NormalMap::getData (imagetexture.cpp:95-115): the
+// texel (int)(u W), (int)(v H), repeated (C++ %) or clamped.  eval's bilinear
+// weights are uv*W - (float)(uv*W) = 0 (imagetexture.cpp:118-134), so eval is
+// this one texel.  A negative coordinate under "repeat" indexes before the
+// image in the reference (undefined); it is wrapped into range here.
+ND uint32_t texel_at(const uint32_t *img, int W, int H, int wrap, V2 uv) {
+    const float x = uv.x * (float)W, y = uv.y * (float)H;
+    int ix, iy;
+    if (wrap == NORI_WRAP_REPEAT) {
+        ix = (int)x % W;
+        iy = (int)y % H;
+        ix += ix < 0 ? W : 0;
+        iy += iy < 0 ? H : 0;
+    } else {
+        ix = min(max((int)x, 0), W - 1);
+        iy = min(max((int)y, 0), H - 1);
+    }
+    return img[(size_t)iy * W + ix];
+}
+// static_cast<float>(byte) / UCHAR_MAX per channel
+ND V3 texel_rgb(uint32_t t) {
+    return V3{(float)(t & 255u) / 255.0f, (float)((t >> 8) & 255u) / 255.0f, (float)((t >> 16) & 255u) / 255.0f};
+}
 
 struct BRec {
     V3 wi, wo;
@@ -239,9 +265,10 @@ struct BRec {
     V2 uv;  // bsdf.h:55, the hit's texture coordinates
 };
 
-// Texture<Color3f>::eval: constant (consttexture.cpp) or Checkerboard::eval
-// (checkerboard.cpp:22-27)
+// Texture<Color3f>::eval: constant (consttexture.cpp), Checkerboard::eval
+// (checkerboard.cpp:22-27) or ImageTexture::eval (imagetexture.cpp:118-134)
 ND V3 albedo_at(const DevBsdf &b, V2 uv) {
+    if (b.tex == NORI_TEXTURE_IMAGE) return texel_rgb(texel_at(b.img, b.img_w, b.img_h, b.img_wrap, uv));
     if (b.tex != NORI_TEXTURE_CHECKERBOARD) return V3{b.albedo[0], b.albedo[1], b.albedo[2]};
     const int x = (int)fabsf(floorf(uv.x / b.tex_scale[0] - b.tex_delta[0]));
     const int y = (int)fabsf(floorf(uv.y / b.tex_scale[1] - b.tex_delta[1]));

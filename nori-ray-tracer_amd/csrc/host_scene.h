@@ -47,6 +47,8 @@ struct HostScene {
     std::vector<nori_bsdf_desc> bsdfs;
     std::vector<nori_emitter_desc> emitters;
     std::vector<std::vector<float>> env_images;  // envmap texels, owned here (emitters[i].env_rgb)
+    std::vector<std::vector<uint8_t>> image_rgb;   // ImageTexture / NormalMap texels (images[i].rgb)
+    std::vector<nori_image_desc> images;
     nori_scene_desc desc{};
     float root_min[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float root_max[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
@@ -60,6 +62,9 @@ struct HostScene {
     void finalize();
 };
 HostScene *load_scene_xml(const std::string &path, int width, int height, int spp);
+// stbi_load(path, .., STBI_rgb) of the reference's stb_image v1.39: baseline
+// JPEG or 8-bit PNG -> width x height x 3 bytes (image_decode.cpp); throws.
+void decode_image_rgb8(const std::string &path, int &width, int &height, std::vector<uint8_t> &rgb);
 // R, G, B planes of an OpenEXR file, rows = image height (image_io.cpp); throws NoriException.
 int load_exr(const std::string &path, int &width, int &height, std::vector<float> &rgb);
 

@@ -868,7 +868,7 @@ ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, 
     const DevShape &sh = S.shapes[h.shape];
     // only a textured albedo reads the texture coordinates (BRec.uv): the
     // sphere's atan2/acos are skipped for every other BSDF
-    const bool need_uv = S.bsdfs[sh.bsdf].tex != NORI_TEXTURE_CONSTANT;
+    const bool need_uv = S.bsdfs[sh.bsdf].tex != NORI_TEXTURE_CONSTANT || sh.nmap;
     h.uv = V2{u, v};
     if (sh.type == NORI_SHAPE_SPHERE) {
         h.p = o + d * t;
@@ -894,6 +894,11 @@ ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, 
         if (sh.has_normals) {
             V3 n = (ld3(S.nrm[i0]) * bx + ld3(S.nrm[i1]) * u) + ld3(S.nrm[i2]) * v;
             h.sh = frame_from(normalize(n));
+            if (sh.nmap) {  // NormalMap::eval (normalmap.cpp:95-134): 2 * byte / 255 - 1, normalized
+                const V3 t = texel_rgb(texel_at(sh.nmap, sh.nm_w, sh.nm_h, sh.nm_wrap, h.uv));
+                const V3 m = V3{2.0f * t.x - 1.0f, 2.0f * t.y - 1.0f, 2.0f * t.z - 1.0f};
+                h.sh = frame_from(to_world(h.sh, normalize(m)));
+            }
         } else {
             h.sh = frame_from(normalize(cross(p1 - p0, p2 - p0)));
         }

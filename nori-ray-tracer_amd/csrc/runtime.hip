@@ -193,6 +193,7 @@ struct nori_gpu_ctx {
     DevScene S{};
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob;
+    DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
     uint32_t spp = 1;    // the scene's sampleCount (default pass count)
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
     uint32_t bvh_depth = 0, bvh_nodes = 0, num_prims = 0;
@@ -284,6 +285,28 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
             rmax[k] = std::fmax(rmax[k], p[k]);
         }
     };
+    // image textures and normal maps: 8-bit RGB -> one RGBX word per texel, so
+    // a lookup is one 4-byte load; DevBsdf/DevShape hold pointers into it
+    std::vector<size_t> img_off(d.num_images);
+    {
+        std::vector<uint32_t> tex;
+        for (uint32_t i = 0; i < d.num_images; ++i) {
+            const nori_image_desc &im = d.images[i];
+            if (!im.rgb || im.width <= 0 || im.height <= 0 || (im.wrap != NORI_WRAP_REPEAT && im.wrap != NORI_WRAP_CLAMP))
+                throw NoriException(NORI_ERR_INVALID, "bad image description");
+            img_off[i] = tex.size();
+            const size_t n = (size_t)im.width * im.height;
+            for (size_t t = 0; t < n; ++t)
+                tex.push_back((uint32_t)im.rgb[3 * t] | ((uint32_t)im.rgb[3 * t + 1] << 8) | ((uint32_t)im.rgb[3 * t + 2] << 16));
+        }
+        if (tex.empty()) tex.assign(1, 0u);
+        c.tex.upload(tex);
+    }
+    auto image_ptr = [&](int32_t i) -> const uint32_t * {
+        if (i < 0) return nullptr;
+        if ((uint32_t)i >= d.num_images) throw NoriException(NORI_ERR_INVALID, "image index out of range");
+        return c.tex.as<uint32_t>() + img_off[i];
+    };
     std::vector<DevShape> shapes(d.num_shapes);
     std::vector<uint32_t> prim_shape, tri_vidx;
     std::vector<float> cdf;
@@ -292,6 +315,12 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         const nori_shape_desc &sd = d.shapes[s];
         DevShape &ds = shapes[s];
         std::memset(&ds, 0, sizeof(ds));
+        ds.nmap = image_ptr(sd.normal_map);
+        if (ds.nmap) {
+            ds.nm_w = d.images[sd.normal_map].width;
+            ds.nm_h = d.images[sd.normal_map].height;
+            ds.nm_wrap = d.images[sd.normal_map].wrap;
+        }
         ds.type = sd.type;
         ds.bsdf = sd.bsdf;
         ds.emitter = sd.emitter;
@@ -373,8 +402,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         o.tex = b.albedo_texture;
         for (int k = 0; k < 3; ++k) o.tex_v2[k] = b.tex_value2[k];
         for (int k = 0; k < 2; ++k) o.tex_delta[k] = b.tex_delta[k], o.tex_scale[k] = b.tex_scale[k];
-        if (b.albedo_texture != NORI_TEXTURE_CONSTANT && b.albedo_texture != NORI_TEXTURE_CHECKERBOARD)
+        if (b.albedo_texture == NORI_TEXTURE_IMAGE) {
+            o.img = image_ptr(b.albedo_image);
+            if (!o.img) throw NoriException(NORI_ERR_INVALID, "ImageTexture albedo without an image");
+            o.img_w = d.images[b.albedo_image].width;
+            o.img_h = d.images[b.albedo_image].height;
+            o.img_wrap = d.images[b.albedo_image].wrap;
+        } else if (b.albedo_texture != NORI_TEXTURE_CONSTANT && b.albedo_texture != NORI_TEXTURE_CHECKERBOARD) {
             throw NoriException(NORI_ERR_INVALID, "unknown albedo texture");
+        }
         if (b.type < NORI_BSDF_DIFFUSE || b.type > NORI_BSDF_DISNEY) throw NoriException(NORI_ERR_INVALID, "unknown bsdf type");
     }
     std::vector<DevEmitter> emitters(d.num_emitters);
@@ -1239,6 +1275,19 @@ int nori_denoise(int device, const float *rgb, const float *variance, int width,
     });
 }
 int nori_gpu_abi_version(void) { return NORI_GPU_ABI_VERSION; }
+
+int nori_read_image(const char *path, int *width, int *height, uint8_t *rgb) {
+    return guarded([&] {
+        if (!path || !width || !height) return fail(NORI_ERR_INVALID, "null argument");
+        int w = 0, h = 0;
+        std::vector<uint8_t> img;
+        decode_image_rgb8(path, w, h, img);
+        *width = w;
+        *height = h;
+        if (rgb) std::memcpy(rgb, img.data(), img.size());
+        return NORI_OK;
+    });
+}
 
 int nori_scene_load_xml(const char *path, int width, int height, int spp, nori_scene **out) {
     return guarded([&] {

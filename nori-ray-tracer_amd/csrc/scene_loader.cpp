@@ -362,8 +362,7 @@ struct Registrar {
 struct Unsupported : NoriObject {
     EClassType getClassType() const override { return EClassTypeCount; }
 };
-static const char *kUnsupported[] = {"checkerboard_float", "image_texture", "normal_map", "perlin",
-                                     "chi2test"};
+static const char *kUnsupported[] = {"checkerboard_float", "perlin", "chi2test"};
 
 // ---- textures (consttexture.cpp)
 struct ConstantColor : NoriObject {
@@ -389,10 +388,39 @@ struct CheckerboardColor : NoriObject {  // checkerboard.cpp:62-68 (Checkerboard
     EClassType getClassType() const override { return ETexture; }
 };
 NORI_REGISTER_CLASS(CheckerboardColor, "checkerboard_color")
+// ImageTexture (imagetexture.cpp:69-85) and NormalMap (normalmap.cpp:69-85):
+// "fileName" (default textures/default.png, resolved against the scene's
+// directory) decoded at construction like stbi_load(.., STBI_rgb), "wrap"
+// repeat | clamp (common.h:274-283).  Evaluated on the device (albedo_at,
+// surface) and by the oracle.
+struct ImageTex : NoriObject {
+    bool normal_map;
+    int width = 0, height = 0, wrap = NORI_WRAP_REPEAT;
+    std::vector<uint8_t> rgb;
+    ImageTex(const PropertyList &p, bool nm) : normal_map(nm) {
+        const std::string file = p.getString("fileName", "textures/default.png");
+        const std::string w = p.getString("wrap", "repeat");
+        if (w == "repeat") wrap = NORI_WRAP_REPEAT;
+        else if (w == "clamp") wrap = NORI_WRAP_CLAMP;
+        else throw NoriException(NORI_ERR_PARSE, "Invalid wrap type name " + w);
+        if (file.empty()) throw NoriException(NORI_ERR_PARSE, "No image data was loaded!");
+        decode_image_rgb8(resolve_path(file), width, height, rgb);
+    }
+    EClassType getClassType() const override { return ETexture; }
+};
+struct ImageTexture : ImageTex {
+    explicit ImageTexture(const PropertyList &p) : ImageTex(p, false) {}
+};
+NORI_REGISTER_CLASS(ImageTexture, "ImageTexture")
+struct NormalMap : ImageTex {
+    explicit NormalMap(const PropertyList &p) : ImageTex(p, true) {}
+};
+NORI_REGISTER_CLASS(NormalMap, "NormalMap")
 
 // ---- BSDFs
 struct Bsdf : NoriObject {
     nori_bsdf_desc d{};
+    const ImageTex *image = nullptr;  // diffuse ImageTexture albedo
     // consumed children (textures) stay alive until the BSDF dies: the parser
     // calls setParent on a child after addChild (parser.cpp:208-211)
     std::vector<std::unique_ptr<NoriObject>> consumed;
@@ -415,6 +443,10 @@ struct Diffuse : Bsdf {  // diffuse.cpp:29-66
         if (has_albedo) throw NoriException(NORI_ERR_PARSE, "There is already an albedo defined!");
         if (auto *c = dynamic_cast<ConstantColor *>(o)) {
             d.albedo[0] = c->value.x; d.albedo[1] = c->value.y; d.albedo[2] = c->value.z;
+        } else if (auto *t = dynamic_cast<ImageTex *>(o)) {
+            d.albedo_texture = NORI_TEXTURE_IMAGE;  // (a NormalMap named "albedo" evaluates its own way)
+            if (t->normal_map) throw NoriException(NORI_ERR_UNSUPPORTED, "a NormalMap as a diffuse albedo");
+            image = t;
         } else if (auto *k = dynamic_cast<CheckerboardColor *>(o)) {
             d.albedo_texture = NORI_TEXTURE_CHECKERBOARD;
             d.albedo[0] = k->value1.x; d.albedo[1] = k->value1.y; d.albedo[2] = k->value1.z;
@@ -422,7 +454,7 @@ struct Diffuse : Bsdf {  // diffuse.cpp:29-66
             d.tex_delta[0] = k->delta[0]; d.tex_delta[1] = k->delta[1];
             d.tex_scale[0] = k->scale[0]; d.tex_scale[1] = k->scale[1];
         } else {
-            throw NoriException(NORI_ERR_UNSUPPORTED, "albedo textures: constant_color and checkerboard_color are on this path");
+            throw NoriException(NORI_ERR_UNSUPPORTED, "albedo textures: constant_color, checkerboard_color and ImageTexture are on this path");
         }
         has_albedo = true;
         consumed.emplace_back(o);
@@ -533,6 +565,8 @@ NORI_REGISTER_CLASS(SpotEmitter, "spotlight")
 struct Shape : NoriObject {
     NoriObject *bsdf = nullptr;
     Emitter *emitter = nullptr;
+    ImageTex *normal_map = nullptr;
+    std::vector<std::unique_ptr<NoriObject>> textures;  // textures added as children stay alive with the shape
     EClassType getClassType() const override { return EMesh; }
     ~Shape() override { delete bsdf; }
     void addChild(NoriObject *o) override {  // shape.cpp:42-74
@@ -545,8 +579,15 @@ struct Shape : NoriObject {
             if (emitter) throw NoriException(NORI_ERR_PARSE, "Shape: tried to register multiple Emitter instances!");
             emitter = static_cast<Emitter *>(o);
             break;
-        case ETexture:
-            throw NoriException(NORI_ERR_UNSUPPORTED, "normal maps are not on this path");
+        case ETexture:  // shape.cpp:59-67: a texture named "normal" is the normal map, others are ignored
+            if (o->idName == "normal") {
+                if (normal_map) throw NoriException(NORI_ERR_PARSE, "Shape: tried to register multiple Normal map instances!");
+                auto *t = dynamic_cast<ImageTex *>(o);
+                if (!t || !t->normal_map) throw NoriException(NORI_ERR_UNSUPPORTED, "normal maps: NormalMap textures only");
+                normal_map = t;
+            }
+            textures.emplace_back(o);
+            break;
         default:
             throw NoriException(NORI_ERR_PARSE, std::string("Shape::addChild(<") + class_name(o->getClassType()) + ">) is not supported!");
         }
@@ -1075,12 +1116,24 @@ HostScene *load_scene_xml(const std::string &path, int width, int height, int sp
 
     auto hs = std::make_unique<HostScene>();
     hs->source = path;
+    std::vector<const ImageTex *> image_src;  // one images[] entry per texture object
+    auto add_image = [&](const ImageTex *t) -> int32_t {
+        for (size_t i = 0; i < image_src.size(); ++i)
+            if (image_src[i] == t) return (int32_t)i;
+        image_src.push_back(t);
+        hs->image_rgb.push_back(t->rgb);
+        hs->images.push_back(nori_image_desc{t->width, t->height, t->wrap, nullptr});
+        return (int32_t)(image_src.size() - 1);
+    };
     for (size_t si = 0; si < sc->shapes.size(); ++si) {
         Shape *sh = sc->shapes[si];
         nori_shape_desc d{};
         d.emitter = -1;
+        d.normal_map = sh->normal_map ? add_image(sh->normal_map) : -1;
         d.bsdf = (int32_t)hs->bsdfs.size();
-        hs->bsdfs.push_back(static_cast<Bsdf *>(sh->bsdf)->d);
+        const Bsdf *bo = static_cast<Bsdf *>(sh->bsdf);
+        hs->bsdfs.push_back(bo->d);
+        hs->bsdfs.back().albedo_image = bo->image ? add_image(bo->image) : -1;
         if (auto *m = dynamic_cast<WavefrontOBJ *>(sh)) {
             d.type = NORI_SHAPE_MESH;
             d.vtx_offset = (uint32_t)(hs->positions.size() / 3);
@@ -1174,6 +1227,9 @@ void HostScene::finalize() {
     desc.bsdfs = bsdfs.data();
     desc.num_emitters = (uint32_t)emitters.size();
     desc.emitters = emitters.data();
+    for (size_t i = 0; i < images.size(); ++i) images[i].rgb = image_rgb[i].data();
+    desc.num_images = (uint32_t)images.size();
+    desc.images = images.data();
 }
 
 }  // namespace nori

@@ -26,7 +26,7 @@ from ._abi import NoriError, check, lib  # noqa: F401
 
 __all__ = ["load_scene", "Scene", "GpuRenderer", "RenderThread", "NoriError", "device_count",
            "develop", "write_exr", "write_png", "read_exr", "film_variance", "ldr_bytes", "variance_gray",
-           "denoise"]
+           "denoise", "read_image"]
 
 
 def _fptr(a):
@@ -206,6 +206,17 @@ def read_exr(path):
     check(lib().nori_read_exr(os.fsencode(path), C.byref(w), C.byref(h), None))
     out = np.zeros((h.value, w.value, 3), np.float32)
     check(lib().nori_read_exr(os.fsencode(path), C.byref(w), C.byref(h), _fptr(out)))
+    return out
+
+
+def read_image(path):
+    """An image texture file decoded like the reference's stbi_load(.., STBI_rgb): (height, width, 3) uint8
+    (nori_read_image; baseline JPEG or 8-bit PNG)."""
+    w, h = C.c_int(), C.c_int()
+    check(lib().nori_read_image(os.fsencode(path), C.byref(w), C.byref(h), None))
+    out = np.zeros((h.value, w.value, 3), np.uint8)
+    check(lib().nori_read_image(os.fsencode(path), C.byref(w), C.byref(h),
+                                out.ctypes.data_as(C.POINTER(C.c_uint8))))
     return out
 
 

@@ -6,7 +6,7 @@ test suite checks their sizes against the library (tests/test_abi.py).
 import ctypes as C
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 NORI_OK = 0
 NORI_ERR_INVALID = -1
@@ -20,7 +20,8 @@ NORI_ERR_OOM = -7
 SHAPE_MESH, SHAPE_SPHERE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET, BSDF_DISNEY = range(5)
 EMITTER_AREA, EMITTER_ENVMAP, EMITTER_POINT, EMITTER_SPOT = 0, 1, 2, 3
-TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD = 0, 1
+TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD, TEXTURE_IMAGE = 0, 1, 2
+WRAP_REPEAT, WRAP_CLAMP = 0, 1
 CAMERA_PERSPECTIVE, CAMERA_THINLENS, CAMERA_ADVANCED = 0, 1, 2
 (INTEGRATOR_PATH_MATS, INTEGRATOR_PATH_MIS, INTEGRATOR_VOLUMETRIC, INTEGRATOR_NORMALS, INTEGRATOR_AV,
  INTEGRATOR_DIRECT, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS,
@@ -36,7 +37,12 @@ class ShapeDesc(C.Structure):
     _fields_ = [("type", C.c_int32), ("tri_offset", C.c_uint32), ("tri_count", C.c_uint32),
                 ("vtx_offset", C.c_uint32), ("vtx_count", C.c_uint32), ("has_normals", C.c_int32),
                 ("has_uvs", C.c_int32), ("center", C.c_float * 3), ("radius", C.c_float),
-                ("bsdf", C.c_int32), ("emitter", C.c_int32)]
+                ("bsdf", C.c_int32), ("emitter", C.c_int32), ("normal_map", C.c_int32)]
+
+
+class ImageDesc(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("wrap", C.c_int32),
+                ("rgb", C.POINTER(C.c_uint8))]
 
 
 class BsdfDesc(C.Structure):
@@ -45,7 +51,7 @@ class BsdfDesc(C.Structure):
                 ("base_color", C.c_float * 3), ("metallic", C.c_float), ("specular", C.c_float),
                 ("roughness", C.c_float), ("sheen", C.c_float), ("sheen_tint", C.c_float),
                 ("specular_tint", C.c_float), ("albedo_texture", C.c_int32), ("tex_value2", C.c_float * 3),
-                ("tex_delta", C.c_float * 2), ("tex_scale", C.c_float * 2)]
+                ("tex_delta", C.c_float * 2), ("tex_scale", C.c_float * 2), ("albedo_image", C.c_int32)]
 
 
 class EmitterDesc(C.Structure):
@@ -80,7 +86,8 @@ class SceneDesc(C.Structure):
                 ("bsdfs", C.POINTER(BsdfDesc)), ("num_emitters", C.c_uint32),
                 ("emitters", C.POINTER(EmitterDesc)), ("camera", CameraDesc),
                 ("medium", MediumDesc), ("integrator", C.c_int32), ("sample_count", C.c_uint32),
-                ("av_length", C.c_float), ("photon_count", C.c_uint32), ("photon_radius", C.c_float)]
+                ("av_length", C.c_float), ("photon_count", C.c_uint32), ("photon_radius", C.c_float),
+                ("num_images", C.c_uint32), ("images", C.POINTER(ImageDesc))]
 
 
 class RenderDesc(C.Structure):
@@ -123,6 +130,7 @@ SIGNATURES = {
     "nori_denoise": (C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int,
                                C.c_int, C.c_float, C.c_int, C.POINTER(C.c_float)]),
     "nori_read_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)]),
+    "nori_read_image": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint8)]),
     "nori_scene_bvh_info": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nori_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nori_gpu_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),

@@ -226,11 +226,53 @@ typedef struct {
     V3 kd;
     /* disney */
     V3 base; float metallic, specular, roughness, sheen, sheen_tint, spec_tint, d_alpha;
-    /* diffuse albedo texture: constant (albedo) or checkerboard (albedo = value1) */
+    /* diffuse albedo texture: constant (albedo), checkerboard (albedo = value1) or image */
     int tex; V3 tex_v2; float tex_delta[2], tex_scale[2];
+    const nori_image_desc *img;
 } Bsdf;
 
-static void bsdf_init(Bsdf *b, const nori_bsdf_desc *d) {
+/* ImageTexture::getData (imagetexture.cpp:95-115) / NormalMap::getData
+ * (normalmap.cpp:95-115) without the final mapping: the three bytes / 255 of
+ * texel (int)xy, repeated with C's % or clamped.  A negative coordinate under
+ * "repeat" indexes before the image in the reference (undefined behaviour);
+ * it is wrapped into range here, as on the GPU. */
+static V3 image_get_data(const nori_image_desc *im, V2 xy) {
+    int x, y;
+    if (im->wrap == NORI_WRAP_REPEAT) {
+        x = ((int)xy.x) % im->width;
+        y = ((int)xy.y) % im->height;
+        if (x < 0) x += im->width;
+        if (y < 0) y += im->height;
+    } else {
+        x = (int)xy.x; y = (int)xy.y;
+        x = x < 0 ? 0 : (x > im->width - 1 ? im->width - 1 : x);
+        y = y < 0 ? 0 : (y > im->height - 1 ? im->height - 1 : y);
+    }
+    const uint8_t *t = im->rgb + 3 * ((size_t)x + (size_t)im->width * y);
+    return v3((float)t[0] / 255, (float)t[1] / 255, (float)t[2] / 255);
+}
+/* ImageTexture::eval / NormalMap::eval (imagetexture.cpp:118-134): the
+ * reference's "bilinear" form, restated literally (its weights are
+ * uv*W - (float)(uv*W) = 0); `normal` maps each texel to 2 v - 1 first. */
+static V3 image_eval(const nori_image_desc *im, V2 uv, int normal) {
+    float x = uv.x * im->width, y = uv.y * im->height;
+    V2 q00 = {x, y}, q01 = {x, y + 1.0f}, q10 = {x + 1.0f, y}, q11 = {x + 1.0f, y + 1.0f};
+    V3 v00 = image_get_data(im, q00), v01 = image_get_data(im, q01),
+       v10 = image_get_data(im, q10), v11 = image_get_data(im, q11);
+    if (normal) {
+        V3 *c[4] = {&v00, &v01, &v10, &v11};
+        for (int k = 0; k < 4; ++k)
+            *c[k] = v3(2.0f * c[k]->x - 1.0f, 2.0f * c[k]->y - 1.0f, 2.0f * c[k]->z - 1.0f);
+    }
+    float dstdx = uv.x * im->width - x;
+    float dstdy = uv.y * im->height - y;
+    V3 r = vmuls(v00, (1.0f - dstdx) * (1.0f - dstdy));
+    r = vadd(r, vmuls(v01, (1.0f - dstdx) * dstdy));
+    r = vadd(r, vmuls(v10, dstdx * (1.0f - dstdy)));
+    return vadd(r, vmuls(v11, dstdx * dstdy));
+}
+
+static void bsdf_init(Bsdf *b, const nori_bsdf_desc *d, const nori_scene_desc *sd) {
     memset(b, 0, sizeof(*b));
     b->type = d->type;
     b->albedo = v3(d->albedo[0], d->albedo[1], d->albedo[2]);
@@ -248,11 +290,14 @@ static void bsdf_init(Bsdf *b, const nori_bsdf_desc *d) {
     b->tex_v2 = v3(d->tex_value2[0], d->tex_value2[1], d->tex_value2[2]);
     b->tex_delta[0] = d->tex_delta[0]; b->tex_delta[1] = d->tex_delta[1];
     b->tex_scale[0] = d->tex_scale[0]; b->tex_scale[1] = d->tex_scale[1];
+    b->img = (d->albedo_texture == NORI_TEXTURE_IMAGE && sd && d->albedo_image >= 0 &&
+              (uint32_t)d->albedo_image < sd->num_images) ? &sd->images[d->albedo_image] : NULL;
 }
 
 /* Texture<Color3f>::eval(uv): ConstantTexture (consttexture.cpp) or
  * Checkerboard::eval (checkerboard.cpp:22-27) */
 static inline V3 albedo_at(const Bsdf *b, V2 uv) {
+    if (b->tex == NORI_TEXTURE_IMAGE) return image_eval(b->img, uv, 0);
     if (b->tex != NORI_TEXTURE_CHECKERBOARD) return b->albedo;
     int x = (int)fabsf(floorf(uv.x / b->tex_scale[0] - b->tex_delta[0]));
     int y = (int)fabsf(floorf(uv.y / b->tex_scale[1] - b->tex_delta[1]));
@@ -513,6 +558,7 @@ typedef struct {
     int has_normals, has_uvs;
     V3 center; float radius;
     int bsdf, emitter;
+    const nori_image_desc *nmap;        /* NormalMap (shape.cpp:59-67) or NULL */
     /* mesh area DiscretePDF (mesh.cpp:30-38, dpdf.h) */
     float *cdf; float normalization;
     BBox bbox;
@@ -802,6 +848,8 @@ static void set_hit_info(const oracle_scene *s, int si, uint32_t local, const Ra
     if (sh->has_normals) {
         V3 n = vadd(vadd(vmuls(nrm(s, i0), bx), vmuls(nrm(s, i1), by)), vmuls(nrm(s, i2), bz));
         its->sh = frame_from(vnormalize(n));
+        if (sh->nmap)  /* mesh.cpp:149-155 */
+            its->sh = frame_from(to_world(&its->sh, vnormalize(image_eval(sh->nmap, its->uv, 1))));
     } else {
         its->sh = its->geo;
     }
@@ -1711,6 +1759,7 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
         sh->has_uvs = sd->has_uvs;
         sh->center = v3(sd->center[0], sd->center[1], sd->center[2]); sh->radius = sd->radius;
         sh->bsdf = sd->bsdf; sh->emitter = sd->emitter;
+        sh->nmap = (sd->normal_map >= 0 && (uint32_t)sd->normal_map < d->num_images) ? &d->images[sd->normal_map] : NULL;
         sh->prim_offset = off;
         sh->bbox = bbox_empty();
         if (sd->type == NORI_SHAPE_SPHERE) {
@@ -1743,7 +1792,7 @@ int oracle_scene_create(const nori_scene_desc *d, oracle_scene **out) {
     }
     s->nprims = off;
     s->bsdfs = (Bsdf *)calloc(d->num_bsdfs ? d->num_bsdfs : 1, sizeof(Bsdf));
-    for (uint32_t i = 0; i < d->num_bsdfs; ++i) bsdf_init(&s->bsdfs[i], &d->bsdfs[i]);
+    for (uint32_t i = 0; i < d->num_bsdfs; ++i) bsdf_init(&s->bsdfs[i], &d->bsdfs[i], d);
     s->nemitters = d->num_emitters;
     s->emitters = (Emitter *)calloc(d->num_emitters ? d->num_emitters : 1, sizeof(Emitter));
     for (uint32_t i = 0; i < d->num_emitters; ++i) {
@@ -2079,7 +2128,7 @@ int oracle_scene_ttest(const oracle_scene *s, uint32_t n, double *mean, double *
 /* ttest.cpp:107-145 */
 int oracle_bsdf_ttest(const nori_bsdf_desc *bd, float angle_deg, uint32_t n, double *mean, double *var) {
     if (!bd || !mean || !var) return NORI_ERR_INVALID;
-    Bsdf b; bsdf_init(&b, bd);
+    Bsdf b; bsdf_init(&b, bd, NULL);
     float th = angle_deg * (F_PI / 180.0f);                  /* degToRad, common.h:209 */
     float st, ct, sp, cp;
     sincosf(th, &st, &ct); sincosf(0.0f, &sp, &cp);          /* sphericalDirection, common.cpp:244-255 */
@@ -2099,7 +2148,7 @@ int oracle_bsdf_ttest(const nori_bsdf_desc *bd, float angle_deg, uint32_t n, dou
 }
 
 int oracle_bsdf_sample(const nori_bsdf_desc *bd, const float *wi, const float *u2, uint32_t n, float *out) {
-    Bsdf b; bsdf_init(&b, bd);
+    Bsdf b; bsdf_init(&b, bd, NULL);
     for (uint32_t i = 0; i < n; ++i) {
         BRec br; memset(&br, 0, sizeof(br));
         br.wi = v3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]);
@@ -2112,7 +2161,7 @@ int oracle_bsdf_sample(const nori_bsdf_desc *bd, const float *wi, const float *u
 }
 
 int oracle_bsdf_eval_pdf(const nori_bsdf_desc *bd, const float *wi, const float *wo, uint32_t n, float *out) {
-    Bsdf b; bsdf_init(&b, bd);
+    Bsdf b; bsdf_init(&b, bd, NULL);
     for (uint32_t i = 0; i < n; ++i) {
         BRec br; memset(&br, 0, sizeof(br));
         br.wi = v3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]); br.wo = v3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);

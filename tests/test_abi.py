@@ -34,7 +34,7 @@ def test_struct_layout_matches_c(built, tmp_path):
                "nori_emitter_desc": _abi.EmitterDesc, "nori_camera_desc": _abi.CameraDesc,
                "nori_medium_desc": _abi.MediumDesc, "nori_scene_desc": _abi.SceneDesc,
                "nori_gpu_render_desc": _abi.RenderDesc, "nori_gpu_stats": _abi.Stats,
-               "nori_gpu_hit": _abi.Hit}
+               "nori_gpu_hit": _abi.Hit, "nori_image_desc": _abi.ImageDesc}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
