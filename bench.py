@@ -298,7 +298,7 @@ def main():
             "config": {"workload": label, "scene": os.path.relpath(xml, ROOT) if xml.startswith(ROOT) else
                        os.path.basename(xml), "integrator": scene.integrator,
                        "parallelism": f"{args.shard}-sharded x{world}, RCCL film reduce in libnori_gpu" if world > 1
-                       else "single GPU", "path_pool": args.pool or 4194304},
+                       else "single GPU", "path_pool": last.get("path_pool")},
             "samples_per_step": samples_per_step,
             "invalid_samples": invalid,
             "roofline": roof,

@@ -316,7 +316,7 @@ typedef struct nori_gpu_stats {
     uint32_t bvh_nodes, bvh_depth;
     uint32_t stream_parts;        /* pool parts on their own streams: each kernel
                                      runs stream_parts launches per iteration  */
-    uint32_t reserved;
+    uint32_t path_pool;           /* paths in flight (the pool size used)     */
     double ms_total;              /* render wall time (host timer)              */
     /* with desc.timing: summed HIP-event time of each kernel, on the launch stream */
     double ms_extend, ms_shadow, ms_shade, ms_splat, ms_finish;

@@ -786,11 +786,20 @@ void photon_preprocess(nori_gpu_ctx &c, const nori_scene_desc &d) {
     DevBuf dpre, out;
     dpre.upload(pre);
     out.ensure(48 * (size_t)N);
+    // all-ones (NaN) first: a slot the store pass leaves unwritten keeps a NaN
+    // in its zero pad word and is caught below instead of entering the map
+    HIP_TRY(hipMemsetAsync(out.p, 0xFF, 48 * (size_t)N, c.stream));
     HIP_TRY(launch_photons(c.S, 0, (uint32_t)pre.size(), nullptr, dpre.as<uint64_t>(), N, out.as<float4>(), c.stack,
                            c.stream));
     HIP_TRY(hipStreamSynchronize(c.stream));
     std::vector<float> raw(12 * (size_t)N), ph, tab;
     HIP_TRY(hipMemcpy(raw.data(), out.p, 48 * (size_t)N, hipMemcpyDeviceToHost));
+    // the store pass must reproduce the count pass photon for photon
+    // (position, 0, direction, 0, power, 0 per slot)
+    for (size_t i = 0; i < (size_t)N; ++i)
+        if (!(raw[12 * i + 3] == 0.0f && raw[12 * i + 7] == 0.0f && raw[12 * i + 11] == 0.0f))
+            throw NoriException(NORI_ERR_INVALID, "photonmapper: the store pass left photon slot " + std::to_string(i) +
+                                                      " unwritten (count and store passes disagree)");
     std::vector<uint32_t> start, rgbe;
     uint32_t mask = 0;
     build_photon_map(raw, (uint32_t)N, d.photon_radius, ph, rgbe, tab, start, mask);
@@ -941,13 +950,23 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     if (!one_bounce && (S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f))
         throw NoriException(NORI_ERR_UNSUPPORTED,
                             "chromatic aberration (three rays per sample) is on the one-bounce integrators only");
-    // default pool: 4M paths in flight (~0.9 GB of queues); measured best among
-    // 256K..4M on cbox (larger pools hide the shade kernel's memory latency)
+    // default pool: about 1/16 of the render's samples in flight, between 1M
+    // and 4M paths (~0.9 GB of queues at 4M).  Large pools hide the shade
+    // kernel's memory latency (4M measured best among 256K..4M on cbox at 512
+    // spp); small renders -- the per-GPU share of a strong-scaled frame --
+    // spend less time draining a smaller pool (cbox 64 spp: 4M 2190, 2M 2320,
+    // 1M 2400 Msamples/s; 512 spp: 4M and 2M within 1 %).
     if (one_bounce) return render_one_bounce(c, rd, pixels, blocks, rgbw_out, stats, t0);
     uint32_t pool = rd.path_pool;
     if (!pool) {  // NORI_PATH_POOL: default pool size override (tuning)
         const char *e = std::getenv("NORI_PATH_POOL");
-        pool = e && std::atol(e) > 0 ? (uint32_t)std::min<long>(std::atol(e), 1L << 26) : (1u << 22);
+        if (e && std::atol(e) > 0) {
+            pool = (uint32_t)std::min<long>(std::atol(e), 1L << 26);
+        } else {
+            const uint64_t want = (uint64_t)passes * M / 16;
+            pool = 1u << 20;
+            while (pool < (1u << 22) && pool < want) pool <<= 1;
+        }
     }
     pool = std::max<uint32_t>(kSeg, (pool + kSeg - 1) / kSeg * kSeg);
     ensure_pool(c, pool);
@@ -1198,6 +1217,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         stats->bvh_nodes = c.bvh_nodes;
         stats->bvh_depth = c.bvh_depth;
         stats->stream_parts = parts;
+        stats->path_pool = pool;
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->ms_extend = kms[0];
         stats->ms_shadow = kms[1];
@@ -1260,6 +1280,16 @@ int nori_denoise(int device, const float *rgb, const float *variance, int width,
             patch > 5 || mode < 0 || mode > 1 || !(k > 0.0f))
             return fail(NORI_ERR_INVALID, "nori_denoise: invalid arguments");
         HIP_TRY(hipSetDevice(device));
+        {  // the tile + halo staging must fit one work-group's LDS
+            int lds_max = 0;
+            HIP_TRY(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+            const size_t need = denoise_lds_bytes(radius, patch - 1);
+            if (need > (size_t)lds_max)
+                return fail(NORI_ERR_INVALID, "nori_denoise: radius " + std::to_string(radius) + " / patch " +
+                                                  std::to_string(patch) + " need " + std::to_string(need) +
+                                                  " bytes of LDS per work-group, the device has " +
+                                                  std::to_string(lds_max));
+        }
         const size_t n = (size_t)width * (size_t)height;
         DevBuf di, dv, dout;
         di.ensure(12 * n);

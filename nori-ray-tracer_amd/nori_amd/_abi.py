@@ -102,7 +102,7 @@ class Stats(C.Structure):
                 ("rays_shadow", C.c_uint64), ("rays_finish", C.c_uint64), ("iterations", C.c_uint64),
                 ("scene_bytes", C.c_uint64),
                 ("bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32), ("stream_parts", C.c_uint32),
-                ("reserved", C.c_uint32), ("ms_total", C.c_double),
+                ("path_pool", C.c_uint32), ("ms_total", C.c_double),
                 ("ms_extend", C.c_double), ("ms_shadow", C.c_double), ("ms_shade", C.c_double),
                 ("ms_splat", C.c_double), ("ms_finish", C.c_double)]
 
