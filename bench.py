@@ -52,7 +52,7 @@ from nori_amd._abi import BLOCK_SIZE  # noqa: E402
 
 METRIC = "Msamples/sec on cbox_path_mis 512×512@512spp; per-pixel L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PROFILE = os.path.join(ROOT, "profiles", "pmc_r02.json")  # committed rocprofv3 evidence (tools/pmc_to_profile.py)
+PROFILE_TAG = "r02"  # committed rocprofv3 evidence: profiles/pmc_<tag>[_<config>].json (tools/pmc_to_profile.py)
 VALU_PEAK = 256 * 4 * 2.4e9 / 2 * 64  # lane-instr/s: 256 CUs x 4 SIMDs, a wave64 VALU op per 2 cycles
 
 
@@ -118,10 +118,11 @@ def parity_check(xml, width, height, spp):
             "config": f"{width}x{height}@{spp}spp of the benched scene, identical WAVE streams"}
 
 
-def profiled(prefix):
-    """Per-launch rocprofv3 numbers of the kernel whose name starts with `prefix`, if committed."""
+def profiled(prefix, config="c2"):
+    """Per-launch rocprofv3 numbers of the kernel whose name starts with `prefix`, if committed for this config."""
+    name = f"pmc_{PROFILE_TAG}.json" if config == "c2" else f"pmc_{PROFILE_TAG}_{config}.json"
     try:
-        d = json.load(open(PROFILE))
+        d = json.load(open(os.path.join(ROOT, "profiles", name)))
     except (OSError, ValueError):
         return None
     for k, v in d.get("kernels", {}).items():
@@ -130,7 +131,7 @@ def profiled(prefix):
     return None
 
 
-def roofline(ts, samples):
+def roofline(ts, samples, config="c2"):
     """Per-kernel roofline rows of an isolated (one pool part) timing render.
 
     Algorithmic HBM bytes:
@@ -156,7 +157,7 @@ def roofline(ts, samples):
         row = {"ms_per_step": ms, "launches": launches, "avg_launch_ms": avg, "bytes_per_launch": nbytes / launches,
                "achieved_GBs": nbytes / launches / (avg / 1e3) / 1e9}
         row["frac"] = row["achieved_GBs"] / HBM_PEAK_GBS
-        prof = profiled(name)
+        prof = profiled(name, config)
         if prof:
             row["traffic_bytes_per_launch"] = prof.get("hbm_bytes_per_launch")
             row["rocprof_avg_launch_ms"] = prof.get("trace_avg_ms")
@@ -277,7 +278,7 @@ def main():
         r.render(passes=share[1], pass_begin=share[0], blocks=share[2], path_pool=args.pool, timing=True)
         ts = r.last_stats
         os.environ.pop("NORI_POOL_PARTS")
-        roof = roofline(ts, share_samples)
+        roof = roofline(ts, share_samples, args.config)
     if world > 1:
         dist.barrier()
 
