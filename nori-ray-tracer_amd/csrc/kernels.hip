@@ -1512,6 +1512,9 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
 #ifndef NORI_SHADE_WAVES
 #define NORI_SHADE_WAVES 5
 #endif
+#ifndef NORI_SORT_OCTANT
+#define NORI_SORT_OCTANT 1
+#endif
 // lds_bytes != 0: the scene blob is staged into LDS first, so the chains of
 // dependent table reads of a vertex (shape -> bsdf -> vertices -> light CDF)
 // run at LDS instead of L2 latency.
@@ -1524,6 +1527,10 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
              float4 *rec, Counters *C, uint32_t lds_bytes) {
     static_assert(kShadeBlock == kSeg, "one shade thread per segment slot");
     __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64], s_w[kSeg], s_pix[kSeg];
+#if NORI_SORT_OCTANT
+    __shared__ uint32_t s_oc[8 * (kShadeBlock / 64)];
+    const bool sort_octant = Sg.num_nodes > 0 && Sg.blob_bytes == 0;  // BVH-traversed scenes only
+#endif
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, q = b * kSeg + tid;
 #ifdef NORI_PROF_SHADE  // profiling build: clocks of the kernel's phases, summed over waves
@@ -1587,6 +1594,28 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         al_tot += s_al[w];
         sh_tot += s_sh[w];
     }
+#if NORI_SORT_OCTANT
+    // survivors grouped by the octant of their new direction (then lane
+    // order), so the waves of the BVH extension kernel get rays that visit
+    // a node's children in the same order
+    if (sort_octant) {
+        const uint32_t oct = (ps.d.x < 0.0f ? 1u : 0u) | (ps.d.y < 0.0f ? 2u : 0u) | (ps.d.z < 0.0f ? 4u : 0u);
+        uint32_t mine = 0;
+        for (uint32_t o = 0; o < 8; ++o) {
+            const uint64_t m = __ballot(alive && oct == o);
+            if (lane_id() == 0) s_oc[o * (kShadeBlock / 64) + wave] = (uint32_t)__popcll(m);
+            if (alive && oct == o) mine = rank_in(m);
+        }
+        __syncthreads();
+        if (alive) {
+            uint32_t off = mine;
+            for (uint32_t o = 0; o < 8; ++o)
+                for (uint32_t w = 0; w < kShadeBlock / 64; ++w)
+                    off += (o < oct || (o == oct && w < wave)) ? s_oc[o * (kShadeBlock / 64) + w] : 0u;
+            al_off = off;
+        }
+    }
+#endif
     const uint32_t need_tot = kSeg - al_tot;
     if (so.emit) {
         uint32_t i = b * kSeg + sh_off;
