@@ -138,8 +138,9 @@ def roofline(ts, samples, config="c2"):
       k_extend: per extension ray read ray_o, ray_d (32 B), write hit (16 B);
                 plus the scene's node + primitive bytes once per launch
       k_shadow: per shadow ray read ray_o, ray_d, payload (48 B) (+ the scene)
-      k_shade : per path read ray_o, ray_d, thr, rng, hit (16 B each) + work (4 B) = 84 B,
-                per surviving path write ray_o, ray_d, thr, rng + work = 68 B,
+      k_shade : per path read ray_o, ray_d, thr, hit (16 B each) + the pcg32 state high
+                word (4 B) + the pixel index its stream increment is recomputed from
+                (4 B) = 72 B, per surviving path write ray_o, ray_d, thr + rng = 52 B,
                 per shadow ray 48 B, per new sample 16 B record + 4 B pixel index
     """
     launches = max(ts["iterations"] * max(ts.get("stream_parts", 1), 1), 1)
@@ -147,7 +148,7 @@ def roofline(ts, samples, config="c2"):
     kern = {
         "k_extend": (ts["ms_extend"], rc * 48 + scene * launches),
         "k_shadow": (ts["ms_shadow"], rs * 48 + scene * launches),
-        "k_shade": (ts["ms_shade"], rc * (84 + 68) + rs * 48 + samples * 20),
+        "k_shade": (ts["ms_shade"], rc * (72 + 52) + rs * 48 + samples * 20),
     }
     rows = {}
     for name, (ms, nbytes) in kern.items():

@@ -8,10 +8,15 @@
 //   pos, nrm   float4[V]     vertex position + texture u / normal + texture v
 //   prim_shape uint32[P]     global primitive -> shape
 //   cdf        float[]       per-mesh area CDFs (DiscretePDF, dpdf.h)
-// Path queues (two, ping-ponged) hold one path per entry:
-//   ray_o float4 (o.xyz, mint)   ray_d float4 (d.xyz, maxt)
-//   hit   float4 (t, prim, u, v) thr   float4 (beta.rgb, previous bsdf pdf | -1)
-//   rng   uint4 (pcg32 state, inc) work  uint32 (sample record index)
+// Path queues (two, ping-ponged) hold one path per entry, 52 B + the hit:
+//   ray_o float4 (o.xyz, previous bsdf pdf | -1; a camera ray: 1/z of its
+//                 camera-space direction, so mint = near/z, maxt = far/z)
+//   ray_d float4 (d.xyz, sample record index | bit 31: camera ray; any
+//                 other ray has mint = Epsilon, maxt = inf)
+//   thr   float4 (beta.rgb, pcg32 state bits 0-31)
+//   rng   uint32 (pcg32 state bits 32-63; the stream increment is
+//                 2 sid + 1 of the sample id, recomputed from the record index)
+//   hit   float4 (t, prim, u, v)
 // Shadow queue: ray_o, ray_d, payload float4 (contribution.rgb, work).
 // Sample records: float4 per camera sample (L.rgb, 0).
 #pragma once
@@ -129,13 +134,13 @@ ND DevScene scene_in_lds(const DevScene &S, const char *lds) {
 }
 
 struct PathQueue {
-    float4 *ray_o;
-    float4 *ray_d;
+    float4 *ray_o;   // (o, prev | camera ray: 1/z)
+    float4 *ray_d;   // (d, work | kCameraRay)
     float4 *hit;
-    float4 *thr;
-    uint4 *rng;     // pcg32 state (x,y) and increment (z,w)
-    uint32_t *work;
+    float4 *thr;     // (beta, pcg32 state low word)
+    uint32_t *rng;   // pcg32 state high word
 };
+constexpr uint32_t kCameraRay = 0x80000000u;  // ray_d.w flag: mint/maxt from the camera clip planes
 
 struct ShadowQueue {
     float4 *ray_o;

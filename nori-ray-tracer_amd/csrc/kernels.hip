@@ -456,6 +456,17 @@ ND uint32_t seg_entry(const SegRange &r, uint32_t i) {
     return (r.s0 + k) * kSeg + (i - base);
 }
 
+// A path queue entry's ray (dev_scene.h PathQueue): camera rays carry 1/z of
+// their camera-space direction (mint = nearClip/z, maxt = farClip/z, as
+// camera_sample computes them); every other path ray is (Epsilon, inf).
+ND void path_ray(const DevScene &S, const float4 &a, const float4 &b, TRay &r) {
+    r.o = ld3(a);
+    r.d = ld3(b);
+    const bool cam = (__float_as_uint(b.w) & kCameraRay) != 0u;
+    r.mint = cam ? S.near_clip * a.w : kEps;
+    r.maxt = cam ? S.far_clip * a.w : INF_F;
+}
+
 // Extension rays: closest hit of every queued path (work-group `bid` of the
 // launch's extension part).
 template <int STACK>
@@ -465,12 +476,8 @@ ND void extend_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt,
     const uint32_t i = (bid % kTraceSlices) * kTraceBlock + threadIdx.x;
     if (i < sr.pre[kTraceGroup]) {
         const uint32_t q = seg_entry(sr, i);
-        float4 a = pq.ray_o[q], b = pq.ray_d[q];
         TRay r;
-        r.o = ld3(a);
-        r.d = ld3(b);
-        r.mint = a.w;
-        r.maxt = b.w;
+        path_ray(S, pq.ray_o[q], pq.ray_d[q], r);
         float t, u, v;
         uint32_t p;
         traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
@@ -628,10 +635,14 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(Dev
                 if (!active && my >= given && my < given + take) {
                     q = seg * kSeg + seg_pos + (my - given);
                     const float4 a = J.ray_o[q], b = J.ray_d[q];
-                    r.o = ld3(a);
-                    r.d = ld3(b);
-                    r.mint = a.w;
-                    r.maxt = b.w;
+                    if (ANY) {  // shadow queue: (o, mint), (d, maxt)
+                        r.o = ld3(a);
+                        r.d = ld3(b);
+                        r.mint = a.w;
+                        r.maxt = b.w;
+                    } else {
+                        path_ray(S, a, b, r);
+                    }
                     if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
                     r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
                     tb = INF_F;
@@ -804,11 +815,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQue
         const uint32_t i = i0 + k * kTraceBlock;
         live[k] = i < n;
         q[k] = seg_entry(sr, live[k] ? i : i0);
-        float4 a = pq.ray_o[q[k]], b = pq.ray_d[q[k]];
-        r[k].o = ld3(a);
-        r[k].d = ld3(b);
-        r[k].mint = a.w;
-        r[k].maxt = b.w;
+        path_ray(S, pq.ray_o[q[k]], pq.ray_d[q[k]], r[k]);
     }
     float t[K], u[K], v[K];
     uint32_t p[K];
@@ -1027,7 +1034,7 @@ ND void sample_surface(const DevScene &S, const DevShape &sh, V2 smp, V3 &p, V3 
 // distortion, uniform-disk lens, per-channel focus shift with chromatic
 // aberration, channel = 0..2 then; -1 otherwise).  Eigen column order.
 ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel, V3 &o, V3 &d, float &mint,
-                      float &maxt) {
+                      float &maxt, float *invz_out = nullptr) {
     const float *m = S.s2c;
     const float qx = px * S.invW, qy = py * S.invH;
     const float r0 = ((m[0] * qx + m[1] * qy) + m[2] * 0.0f) + m[3];
@@ -1088,6 +1095,7 @@ ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel,
            (c[8] * dl.x + c[9] * dl.y) + c[10] * dl.z};
     mint = S.near_clip * invZ;
     maxt = S.far_clip * invZ;
+    if (invz_out) *invz_out = invZ;  // path queue encoding of a camera ray (path_ray)
 }
 
 // ------------------------------------------------------------------ shade + regenerate
@@ -1098,6 +1106,8 @@ struct PathState {
     float prev;  // BSDF pdf of the last bounce; -1: w_mats = 1 (camera ray or discrete lobe)
     Pcg rng;
     uint32_t work;
+    bool cam;    // the ray is a camera ray (stored with invz instead of prev)
+    float invz;  // camera ray: 1/z of its camera-space direction
     V3 L;  // finisher only: the sample's radiance so far (the record, held in registers)
 };
 struct ShadowOut {
@@ -1107,26 +1117,33 @@ struct ShadowOut {
     uint32_t work;
 };
 
-ND void load_path(const PathQueue &Q, uint32_t q, PathState &ps) {
-    float4 ro = Q.ray_o[q], rd = Q.ray_d[q], th = Q.thr[q];
-    uint4 rs = Q.rng[q];
+// Sample id of work id w (render.cpp's (pass, pixel) sample; the pcg32 stream
+// key of wave_seed): pass = w / M of the chunk, pixel = the work list's entry.
+ND uint64_t sample_id(const DevScene &S, const WorkDesc &wd, uint32_t w) {
+    const uint32_t pass = w / wd.M;
+    return (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + wd.pixels[w - pass * wd.M];
+}
+ND void load_path(const DevScene &S, const WorkDesc &wd, const PathQueue &Q, uint32_t q, PathState &ps) {
+    const float4 ro = Q.ray_o[q], rd = Q.ray_d[q], th = Q.thr[q];
+    const uint32_t sh = Q.rng[q];
     ps.o = ld3(ro);
     ps.d = ld3(rd);
-    ps.mint = ro.w;
-    ps.maxt = rd.w;
+    const uint32_t wf = __float_as_uint(rd.w);
+    ps.work = wf & ~kCameraRay;
+    ps.cam = (wf & kCameraRay) != 0u;
+    ps.invz = ro.w;
+    ps.prev = ps.cam ? -1.0f : ro.w;
+    ps.mint = ps.cam ? S.near_clip * ro.w : kEps;
+    ps.maxt = ps.cam ? S.far_clip * ro.w : INF_F;
     ps.beta = ld3(th);
-    ps.prev = th.w;
-    ps.rng.state = ((uint64_t)rs.y << 32) | rs.x;
-    ps.rng.inc = ((uint64_t)rs.w << 32) | rs.z;
-    ps.work = Q.work[q];
+    ps.rng.state = ((uint64_t)sh << 32) | __float_as_uint(th.w);
+    ps.rng.inc = (sample_id(S, wd, ps.work) << 1u) | 1u;  // pcg32 seed(initstate, initseq = sid)
 }
 ND void store_path(const PathQueue &Q, uint32_t i, const PathState &ps) {
-    Q.ray_o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.mint);
-    Q.ray_d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, ps.maxt);
-    Q.thr[i] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, ps.prev);
-    Q.rng[i] = make_uint4((uint32_t)ps.rng.state, (uint32_t)(ps.rng.state >> 32), (uint32_t)ps.rng.inc,
-                          (uint32_t)(ps.rng.inc >> 32));
-    Q.work[i] = ps.work;
+    Q.ray_o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.cam ? ps.invz : ps.prev);
+    Q.ray_d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(ps.work | (ps.cam ? kCameraRay : 0u)));
+    Q.thr[i] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, __uint_as_float((uint32_t)ps.rng.state));
+    Q.rng[i] = (uint32_t)(ps.rng.state >> 32);
 }
 
 // ------------------------------------------------------------------ medium
@@ -1492,7 +1509,8 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t p
     wave_seed(ps.rng, wd.seed, sid);
     V2 jit = next2D(ps.rng);
     const V2 ap = next2D(ps.rng);  // apertureSample (render.cpp:99)
-    camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, -1, ps.o, ps.d, ps.mint, ps.maxt);
+    camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, -1, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
+    ps.cam = true;
     ps.beta = V3{1, 1, 1};
     ps.prev = -1.0f;
     ps.work = w;
@@ -1552,7 +1570,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     const uint32_t cursor = seg.cursor[b];
     const uint4 st0 = seg.stats[b];
     PathState ps;
-    load_path(in, q, ps);
+    load_path(Sg, wd, in, q, ps);
     const float4 hit = in.hit[q];
     // The next kSeg positions of the segment's work stream and their pixels:
     // slot j of the free slots regenerates position cursor + j.  Looked up
@@ -1624,6 +1642,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         sq.payload[i] = make_float4(so.contrib.x, so.contrib.y, so.contrib.z, __uint_as_float(so.work));
     }
     if (TRACE && alive) trace_into(Sg, ps, out.hit + b * kSeg + al_off);
+    ps.cam = false;  // a survivor carries its BSDF-sampled ray (Epsilon, inf)
     if (alive) store_path(out, b * kSeg + al_off, ps);
     NORI_SPHASE(3)
     // ---- regeneration: the free slots [al_tot, kSeg) take the next work ids of
@@ -1719,7 +1738,7 @@ ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, ui
 __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg, int sel, float4 *rec) {
     const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
     if (idx >= seg.cnt[sel][sg]) return;
-    rec[Q.work[sg * kSeg + idx]].w = 1.0f;
+    rec[__float_as_uint(Q.ray_d[sg * kSeg + idx].w) & ~kCameraRay].w = 1.0f;
 }
 
 // Cooperative scan (scan-mode scenes, n <= 64 primitives): the rays of the
@@ -1884,7 +1903,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
     PathState ps;
     float4 h = make_float4(0, 0, 0, 0);
     if (active) {
-        load_path(Q, q, ps);
+        load_path(Sg, wd, Q, q, ps);
         h = Q.hit[q];
         ps.L = ld3(rec[ps.work]);
     }

@@ -201,7 +201,7 @@ struct nori_gpu_ctx {
     std::atomic<int> cancel{0};
     std::atomic<float> progress{1.0f};
     // render state
-    DevBuf q[2][6], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
+    DevBuf q[2][5], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
     DevBuf ptctr;                    // persistent traversal work counters, 4 per part
     DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
     DevBuf ph, ph_rgbe, ph_tab, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
@@ -641,8 +641,7 @@ void ensure_pool(nori_gpu_ctx &c, uint32_t pool) {
         c.q[b][1].ensure(16 * (size_t)pool);
         c.q[b][2].ensure(16 * (size_t)pool);
         c.q[b][3].ensure(16 * (size_t)pool);
-        c.q[b][4].ensure(16 * (size_t)pool);
-        c.q[b][5].ensure(4 * (size_t)pool);
+        c.q[b][4].ensure(4 * (size_t)pool);
     }
     for (int k = 0; k < 3; ++k) c.sq[k].ensure(16 * (size_t)pool);
     for (int k = 0; k < 4; ++k) c.seg[k].ensure(4 * (size_t)(pool / kSeg));
@@ -657,8 +656,7 @@ PathQueue queue_of(nori_gpu_ctx &c, int b) {
     q.ray_d = c.q[b][1].as<float4>();
     q.hit = c.q[b][2].as<float4>();
     q.thr = c.q[b][3].as<float4>();
-    q.rng = c.q[b][4].as<uint4>();
-    q.work = c.q[b][5].as<uint32_t>();
+    q.rng = c.q[b][4].as<uint32_t>();
     return q;
 }
 
@@ -1062,7 +1060,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         auto q_view = [&](const PathQueue &q, uint32_t b0) {
             const size_t e = (size_t)b0 * kSeg;
-            return PathQueue{q.ray_o + e, q.ray_d + e, q.hit + e, q.thr + e, q.rng + e, q.work + e};
+            return PathQueue{q.ray_o + e, q.ray_d + e, q.hit + e, q.thr + e, q.rng + e};
         };
         std::vector<std::array<PathQueue, 2>> Qh(parts);
         std::vector<ShadowQueue> sqh(parts);
