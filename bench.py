@@ -308,6 +308,9 @@ def main():
             "rays_per_sample": {"closest": last["rays_closest"] / share_samples,
                                 "shadow": last["rays_shadow"] / share_samples,
                                 "finisher": last["rays_finish"] / share_samples},
+            # whole-job ray throughput (all ranks' rays over the step time)
+            "grays_per_s": {k: world * last[f"rays_{k}"] / (elapsed / args.steps) / 1e9
+                            for k in ("closest", "shadow", "finish")},
             "wavefront_iterations": last["iterations"],
             "stream_parts": last.get("stream_parts", 1),
             "hip_runtime": hip_runtime(),

@@ -56,6 +56,8 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st);
 // Marks the record of every queued path pending (w = 1): k_splat skips it.
+// Zeroes the counters and segment state of a chunk, Counters::exhausted = empty.
+hipError_t launch_reset(Counters *C, uint32_t empty, const SegState &seg, uint32_t G, hipStream_t st);
 hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st);
 // Completes every queued path and splats its sample into `film` itself.
 // (pre: G + 1 words of scratch for the prefix over the segment counts)

@@ -2566,6 +2566,26 @@ int pt_blocks_per_cu(int stack, bool any) {
     return e == hipSuccess ? n : 0;
 }
 
+// Start of a chunk of passes: zero the counters, the segments' path counts,
+// work cursors and statistics, and preset the count of segments whose work
+// stream is empty from the start (one launch instead of five copies/fills).
+__global__ __launch_bounds__(256) void k_reset(Counters *C, uint32_t empty, SegState seg, uint32_t G) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    constexpr uint32_t nw = sizeof(Counters) / 4;
+    if (i < nw) reinterpret_cast<uint32_t *>(C)[i] = i == 0 ? empty : 0u;  // word 0: exhausted
+    if (i < G) {
+        seg.cnt[0][i] = 0u;
+        seg.cursor[i] = 0u;
+        seg.stats[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+hipError_t launch_reset(Counters *C, uint32_t empty, const SegState &seg, uint32_t G, hipStream_t st) {
+    static_assert(offsetof(Counters, exhausted) == 0, "Counters layout");
+    const uint32_t n = std::max<uint32_t>(G, sizeof(Counters) / 4);
+    hipLaunchKernelGGL(k_reset, dim3((n + 255) / 256), dim3(256), 0, st, C, empty, seg, G);
+    return hipGetLastError();
+}
+
 hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st) {
     hipLaunchKernelGGL(k_mark, dim3(2 * G), dim3(kTraceBlock), 0, st, Q, seg, sel, rec);
     return hipGetLastError();

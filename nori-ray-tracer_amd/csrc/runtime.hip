@@ -209,6 +209,15 @@ struct nori_gpu_ctx {
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
     uint32_t *pinned_dev = nullptr;  // device view of `pinned`
+    // the render's blocks (spiral order, block_subset applied) and their
+    // block-major pixel list, with device copies in `pixels` / `blocks`:
+    // rebuilt and uploaded only when the block selection changes
+    std::vector<uint32_t> work_order, hpixels;
+    std::vector<int4> hblocks;
+    bool work_valid = false;
+    // pinned staging of the end-of-render read-back (Counters + per-segment stats)
+    char *readback = nullptr;
+    size_t readback_bytes = 0;
     std::vector<hipEvent_t> ring[kMaxParts];
     ~nori_gpu_ctx() {
         for (auto &r : ring)
@@ -218,6 +227,7 @@ struct nori_gpu_ctx {
             if (parts[h]) (void)hipStreamDestroy(parts[h]);
         }
         if (pinned) (void)hipHostFree(pinned);
+        if (readback) (void)hipHostFree(readback);
         if (fork) (void)hipEventDestroy(fork);
         if (join) (void)hipEventDestroy(join);
         if (side) (void)hipStreamDestroy(side);
@@ -829,8 +839,6 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
     chunk = (uint32_t)std::min<uint64_t>(chunk, ((uint64_t)1 << 31) / M);
     c.rec.ensure(16 * (size_t)chunk * M);
     c.counters.ensure(sizeof(Counters));
-    c.pixels.upload(pixels);
-    c.blocks.upload(blocks);
     const size_t film_elems = 4 * (size_t)(W + 2 * B) * (H + 2 * B);
     float *film = nullptr;
     if (rd.output_on_device) {
@@ -912,11 +920,12 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
     return NORI_OK;
 }
 
-int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nori_gpu_stats *stats) {
-    auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipSetDevice(c.device));
-    const DevScene &S = c.S;
-    const int W = S.W, H = S.H, B = S.border;
+// The render's blocks in BlockGenerator order (block.cpp:140-188) with the
+// block_subset applied, and the block-major pixel list (camera samples of one
+// block are adjacent work ids); cached on the context with their device
+// copies, so a render of the same selection neither rebuilds nor uploads them.
+static void work_lists(nori_gpu_ctx &c, const nori_gpu_render_desc &rd) {
+    const int W = c.S.W, H = c.S.H;
     const int nbx = (int)std::ceil(W / (float)NORI_BLOCK_SIZE), nby = (int)std::ceil(H / (float)NORI_BLOCK_SIZE);
     std::vector<uint32_t> order = spiral_blocks(W, H);
     if (rd.num_blocks) {
@@ -930,17 +939,32 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             if (want[b]) sel.push_back(b);
         order.swap(sel);
     }
-    // block-major pixel list (camera samples of one block are adjacent work ids)
-    std::vector<uint32_t> pixels;
-    std::vector<int4> blocks;
+    if (c.work_valid && order == c.work_order) return;
+    c.work_valid = false;
+    c.hpixels.clear();
+    c.hblocks.clear();
     for (uint32_t b : order) {
         int bx = (int)(b % (uint32_t)nbx), by = (int)(b / (uint32_t)nbx);
         int ox = bx * NORI_BLOCK_SIZE, oy = by * NORI_BLOCK_SIZE;
         int bw = std::min(NORI_BLOCK_SIZE, W - ox), bh = std::min(NORI_BLOCK_SIZE, H - oy);
-        blocks.push_back(make_int4(ox, oy, bw | (bh << 16), (int)pixels.size()));
+        c.hblocks.push_back(make_int4(ox, oy, bw | (bh << 16), (int)c.hpixels.size()));
         for (int y = 0; y < bh; ++y)
-            for (int x = 0; x < bw; ++x) pixels.push_back((uint32_t)((oy + y) * W + (ox + x)));
+            for (int x = 0; x < bw; ++x) c.hpixels.push_back((uint32_t)((oy + y) * W + (ox + x)));
     }
+    c.pixels.upload(c.hpixels);
+    c.blocks.upload(c.hblocks);
+    c.work_order.swap(order);
+    c.work_valid = true;
+}
+
+int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nori_gpu_stats *stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(c.device));
+    const DevScene &S = c.S;
+    const int W = S.W, H = S.H, B = S.border;
+    work_lists(c, rd);
+    const std::vector<uint32_t> &pixels = c.hpixels;
+    const std::vector<int4> &blocks = c.hblocks;
     const uint32_t M = (uint32_t)pixels.size();
     const uint32_t passes = rd.pass_count ? rd.pass_count : 0;
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
@@ -974,8 +998,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     chunk = (uint32_t)std::min<uint64_t>(chunk, ((uint64_t)1 << 31) / M);
     c.rec.ensure(16 * (size_t)chunk * M);
     c.counters.ensure(sizeof(Counters));
-    c.pixels.upload(pixels);
-    c.blocks.upload(blocks);
     const size_t film_elems = 4 * (size_t)(W + 2 * B) * (H + 2 * B);
     float *film = nullptr;
     if (rd.output_on_device) {
@@ -1044,11 +1066,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         // segments whose stream is empty from the start count as exhausted
         uint32_t empty = 0;
         for (uint32_t b = 0; b < G; ++b) empty += stream_work(wd, b, 0) >= wd.total;
-        HIP_TRY(hipMemsetAsync(C, 0, sizeof(Counters), c.stream));
-        HIP_TRY(hipMemcpyAsync(&C->exhausted, &empty, 4, hipMemcpyHostToDevice, c.stream));
-        HIP_TRY(hipMemsetAsync(seg.cnt[0], 0, 4 * (size_t)G, c.stream));
-        HIP_TRY(hipMemsetAsync(seg.cursor, 0, 4 * (size_t)G, c.stream));
-        HIP_TRY(hipMemsetAsync(seg.stats, 0, 16 * (size_t)G, c.stream));
+        HIP_TRY(launch_reset(C, empty, seg, G, c.stream));
         int last_out = 0;
         // The pool is split into `parts` independent parts (segments never
         // interact), each driven on its own stream: the memory-bound shade
@@ -1149,10 +1167,22 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         });
         HIP_TRY(hipEventRecord(c.join, c.side));
         HIP_TRY(hipStreamWaitEvent(c.stream, c.join, 0));
-        Counters hc;
-        HIP_TRY(hipMemcpyAsync(&hc, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
-        HIP_TRY(hipMemcpyAsync(hstats.data(), seg.stats, 16 * (size_t)G, hipMemcpyDeviceToHost, c.stream));
+        // read-back through pinned staging: both copies queue behind the
+        // finisher without a host round trip each (pageable copies stage twice)
+        const size_t rb = sizeof(Counters) + 16 * (size_t)G;
+        if (c.readback_bytes < rb) {
+            if (c.readback) HIP_TRY(hipHostFree(c.readback));
+            c.readback = nullptr;
+            c.readback_bytes = 0;
+            HIP_TRY(hipHostMalloc((void **)&c.readback, rb, hipHostMallocDefault));
+            c.readback_bytes = rb;
+        }
+        HIP_TRY(hipMemcpyAsync(c.readback, C, sizeof(Counters), hipMemcpyDeviceToHost, c.stream));
+        HIP_TRY(hipMemcpyAsync(c.readback + sizeof(Counters), seg.stats, 16 * (size_t)G, hipMemcpyDeviceToHost, c.stream));
         HIP_TRY(hipStreamSynchronize(c.stream));
+        Counters hc;
+        std::memcpy(&hc, c.readback, sizeof(Counters));
+        std::memcpy(hstats.data(), c.readback + sizeof(Counters), 16 * (size_t)G);
         for (const uint4 &st : hstats) {
             rays_c += st.x;
             rays_s += st.y;
