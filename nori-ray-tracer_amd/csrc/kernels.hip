@@ -1539,7 +1539,11 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
 // TRACE (scan-mode scenes): the closest hit of every outgoing ray is found
 // here as well (wave-uniform scan, traverse<0>), so the rays do not make a
 // round trip through HBM to a separate extension kernel.
-template <int INTEG, bool TRACE>
+// LDS is a template parameter, not a run-time choice: with the scene pointers
+// known to point into LDS the compiler emits ds_read for the table reads; a
+// run-time select between the LDS and the global tables leaves generic
+// pointers, i.e. flat loads (vector-memory latency, both wait counters).
+template <int INTEG, bool TRACE, bool LDS>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
@@ -1580,7 +1584,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     const uint64_t wspec = stream_work(wd, wd.b0 + b, cursor + tid);
     const uint32_t pspec = wspec < wd.total ? wd.pixels[(uint32_t)wspec % wd.M] : 0u;
     DevScene S = Sg;
-    if (lds_bytes) {
+    if constexpr (LDS) {
         for (uint32_t i = tid; i < lds_bytes / 16; i += kShadeBlock) blob_lds[i] = Sg.blob[i];
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
@@ -1862,7 +1866,7 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #ifndef NORI_FINISH_PRIO
 #define NORI_FINISH_PRIO 1
 #endif
-template <int STACK, int INTEG>
+template <int STACK, int INTEG, bool LDS>  // LDS: the scene blob is staged (scan-mode scenes; see k_shade)
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
                                                         const uint32_t *pre, uint32_t G) {
@@ -1877,7 +1881,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
     // tables; for small scenes they are staged into LDS first so the chain
     // runs at LDS latency instead of L2 latency.
     DevScene S = Sg;
-    if (STACK == 0 && Sg.blob_bytes) {  // the BVH path reads global memory (gld)
+    if constexpr (LDS) {  // the BVH path reads global memory (gld)
         for (uint32_t i = threadIdx.x; i < Sg.blob_bytes / 16; i += kTraceBlock) blob_lds[i] = Sg.blob[i];
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
@@ -2470,10 +2474,14 @@ static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQue
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
     dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
-    if (trace)
-        hipLaunchKernelGGL((k_shade<INTEG, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+    if (trace && lds)
+        hipLaunchKernelGGL((k_shade<INTEG, true, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+    else if (trace)
+        hipLaunchKernelGGL((k_shade<INTEG, true, false>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+    else if (lds)
+        hipLaunchKernelGGL((k_shade<INTEG, false, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
-        hipLaunchKernelGGL((k_shade<INTEG, false>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+        hipLaunchKernelGGL((k_shade<INTEG, false, false>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
 }
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
@@ -2598,11 +2606,16 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
     hipLaunchKernelGGL(k_tail_prefix, dim3(1), dim3(1024), 0, st, seg.cnt[sel], G, pre);
     dim3 g(2 * G), b(kTraceBlock);  // enough blocks for a full pool; the idle ones exit at once
     switch (stack) {
-    case 0: hipLaunchKernelGGL((k_finish<0, INTEG>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;  // LDS-staged
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 0:  // LDS-staged when the scene has a blob
+        if (S.blob_bytes)
+            hipLaunchKernelGGL((k_finish<0, INTEG, true>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+        else
+            hipLaunchKernelGGL((k_finish<0, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+        break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
