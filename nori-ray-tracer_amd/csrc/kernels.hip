@@ -1866,6 +1866,10 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #ifndef NORI_FINISH_PRIO
 #define NORI_FINISH_PRIO 1
 #endif
+#ifndef NORI_FINISH_WAVES  // 0: 64 paths per wave
+#define NORI_FINISH_WAVES 8192
+#endif
+constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
 template <int STACK, int INTEG, bool LDS>  // LDS: the scene blob is staged (scan-mode scenes; see k_shade)
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
@@ -1873,10 +1877,14 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
     // the queued paths of all segments, numbered through the prefix `pre`
-    // (k_tail_prefix) so that they fill whole waves: few waves, each with a
-    // SIMD to itself, instead of one or two lanes in thousands of waves
-    const uint32_t n = pre[G], gid = blockIdx.x * kTraceBlock + threadIdx.x;
-    if (blockIdx.x * kTraceBlock >= n) return;  // whole block idle
+    // (k_tail_prefix), K consecutive ones per wave: K = n / kFinishWaves
+    // rounded up, so the tail spreads over about kFinishWaves waves.  The
+    // render waits for the longest path, and a lane's bounce costs the sum of
+    // the branches its wave-mates take: few paths per wave keep that chain
+    // close to the lone-lane latency from its first bounce on.
+    const uint32_t n = pre[G];
+    const uint32_t K = kFinishWaves ? min(64u, max(1u, (n + kFinishWaves - 1) / kFinishWaves)) : 64u;
+    if (blockIdx.x * (kTraceBlock / 64) * K >= n) return;  // whole block idle
     // Each bounce of a tail path is a chain of dependent reads of small
     // tables; for small scenes they are staged into LDS first so the chain
     // runs at LDS latency instead of L2 latency.
@@ -1886,13 +1894,14 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         __syncthreads();
         S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
     }
-    if ((gid & ~63u) >= n) return;  // whole wave idle
+    const uint32_t first = (blockIdx.x * kTraceBlock + threadIdx.x) / 64 * K, gid = first + lane_id();
+    if (first >= n) return;  // whole wave idle
 #if NORI_FINISH_PRIO
     // the film splat runs beside the finisher: its waves must not take the
     // issue slots of these few latency-bound ones
     __builtin_amdgcn_s_setprio(3);
 #endif
-    bool active = gid < n;
+    bool active = lane_id() < K && gid < n;
     uint32_t sg = 0;
     if (active) {  // segment of path gid: last s with pre[s] <= gid
         uint32_t lo = 0, hi = G;
@@ -2604,7 +2613,10 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                             hipStream_t st) {
     hipLaunchKernelGGL(k_tail_prefix, dim3(1), dim3(1024), 0, st, seg.cnt[sel], G, pre);
-    dim3 g(2 * G), b(kTraceBlock);  // enough blocks for a full pool; the idle ones exit at once
+    // enough waves for any path count n <= 256 G (kFinishWaves, or n / 64 <= 4 G when
+    // K = 64); the idle blocks exit at once
+    constexpr uint32_t wpb = kTraceBlock / 64;  // waves per block
+    dim3 g(std::max<uint32_t>(2 * G, (kFinishWaves + wpb - 1) / wpb)), b(kTraceBlock);
     switch (stack) {
     case 0:  // LDS-staged when the scene has a blob
         if (S.blob_bytes)
