@@ -671,7 +671,8 @@ PathQueue queue_of(nori_gpu_ctx &c, int b) {
 }
 
 constexpr int kRing = 16;     // readback ring entries
-constexpr int kLookahead = 6; // iterations queued ahead of the termination check
+constexpr int kLookahead = 6;    // iterations queued ahead of the termination check
+constexpr int kLookaheadEnd = 2; // ... once work streams run dry
 
 struct Timers {
     std::vector<hipEvent_t> ev;
@@ -702,6 +703,13 @@ uint64_t event_every() {  // NORI_EVENT_EVERY: iterations per host event (defaul
     const char *e = std::getenv("NORI_EVENT_EVERY");
     const long v = e ? std::atol(e) : 1;
     return v >= 1 && v <= 8 ? (uint64_t)v : 1;
+}
+// NORI_LOOKAHEAD / NORI_LOOKAHEAD_END: iterations queued ahead of the
+// termination check, before / after the first work stream ran dry
+uint64_t lookahead(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    const long v = e ? std::atol(e) : dflt;
+    return v >= 1 && v <= kRing - 2 ? (uint64_t)v : (uint64_t)dflt;
 }
 bool fused_extend() {
     const char *e = std::getenv("NORI_FUSED_EXTEND");
@@ -1046,7 +1054,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // NORI_FUSED_EXTEND=1: scan-mode scenes trace the extension rays inside
     // the shade kernel (measured even with separate k_extend launches)
     const bool fused = c.stack == 0 && fused_extend();
-    const uint64_t every = event_every();
+    const uint64_t every = event_every(), ahead = lookahead("NORI_LOOKAHEAD", kLookahead),
+                   ahead_end = lookahead("NORI_LOOKAHEAD_END", kLookaheadEnd);
     const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(), pool / kSeg));
     const char *stg = std::getenv("NORI_PART_STAGGER");
     const bool stagger = stg && stg[0] == '1';
@@ -1096,6 +1105,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         HIP_TRY(hipEventRecord(c.fork, c.stream));  // the part streams start after the resets above
         for (uint32_t h = 1; h < parts; ++h) HIP_TRY(hipStreamWaitEvent(c.parts[h], c.fork, 0));
+        uint64_t lag = (ahead + every - 1) / every;
+        const uint64_t lag_end = (ahead_end + every - 1) / every;
         for (uint64_t it = 0;; ++it) {
             int in = (int)(it & 1), out = in ^ 1;
             last_out = out;
@@ -1131,10 +1142,13 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             const uint64_t ev = it / every;
             for (uint32_t h = 0; h < parts; ++h)
                 HIP_TRY(hipEventRecord(c.ring[h][ev % kRing], h ? c.parts[h] : c.stream));
-            const uint64_t lag = (kLookahead + every - 1) / every;
             if (ev >= lag) {
                 for (uint32_t h = 0; h < parts; ++h) HIP_TRY(hipEventSynchronize(c.ring[h][(ev - lag) % kRing]));
                 uint32_t exhausted = __atomic_load_n(&c.pinned[1], __ATOMIC_ACQUIRE);
+                // the streams are running dry: queue fewer iterations ahead,
+                // so that few drain iterations (full-grid launches over a
+                // thinning pool) are already queued when the last one does
+                if (exhausted) lag = std::min(lag, lag_end);
                 c.progress = (float)std::min(1.0, (double)done_before / (double)total_all +
                                                       (double)np / passes * exhausted / G);
                 // every work id has been handed out: finish the remaining paths in one launch
