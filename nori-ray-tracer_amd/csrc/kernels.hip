@@ -778,16 +778,30 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(Dev
 #else
 #define NORI_TRACE_ATTR
 #endif
+// XCD-aware block order for the BVH walks (NORI_XCD_REMAP): the dispatcher
+// sends work-group b to XCD b % 8, each XCD with its own 4 MB L2.  Giving XCD
+// x a contiguous range of queue segments (neighbouring image chunks, so
+// nearby ray origins) lets each L2 hold the part of the tree its rays visit.
+// A bijection of [0, nb): XCD x takes ranks [x q + min(x, r), ... + count).
+#ifndef NORI_XCD_REMAP
+#define NORI_XCD_REMAP 1
+#endif
+constexpr uint32_t kXcds = 8;
+ND uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    if (!NORI_XCD_REMAP) return b;
+    const uint32_t x = b % kXcds, k = b / kXcds, q = nb / kXcds, r = nb % kXcds;
+    return x * q + min(x, r) + k;
+}
 template <int STACK>
 __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_extend(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    extend_body<STACK>(S, pq, cnt, G, blockIdx.x, stk);
+    extend_body<STACK>(S, pq, cnt, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
 template <int STACK>
 __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
                                                         float4 *rec, uint32_t G) {
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    shadow_body<STACK>(S, sq, shcnt, rec, G, blockIdx.x, stk);
+    shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
 // Scan-mode traversal of K rays per thread: every primitive record is
 // fetched once (scalar loads) and tested against K independent rays, which
