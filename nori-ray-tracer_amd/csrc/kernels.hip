@@ -2205,10 +2205,17 @@ struct OneBounce {
     }
 };
 
+#ifndef NORI_DIRECT_XCD
+#define NORI_DIRECT_XCD 1
+#endif
 template <int STACK, int INTEG>
 __global__ __launch_bounds__(kTraceBlock) void k_direct(DevScene S, WorkDesc wd, float4 *rec, Counters *C) {
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    const uint64_t w = (uint64_t)blockIdx.x * kTraceBlock + threadIdx.x;
+    // XCD-aware order (NORI_DIRECT_XCD): each XCD sweeps its own contiguous
+    // eighth of the work ids, so at any moment it shades one band of image
+    // rows and its L2 holds the photons / tree nodes of that band
+    const uint32_t bid = NORI_DIRECT_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t w = (uint64_t)bid * kTraceBlock + threadIdx.x;
     OneBounce<STACK> ob{S, stk + threadIdx.x};
     if (w < wd.total) {
         const uint32_t pass = (uint32_t)(w / wd.M), e = (uint32_t)(w - (uint64_t)pass * wd.M), pix = wd.pixels[e];
