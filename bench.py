@@ -6,8 +6,9 @@ scenes/pa4/cbox/cbox_path_mis.xml, with its mirror and dielectric spheres),
 from resident scene data to the filtered RGBW film in HBM.  --config c3|c4|c5
 benches the other single-GPU-sized BASELINE configs (nori_amd.configs).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one
-process per GPU.  STRONG scaling: the frame is fixed and split over the ranks
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N, or plain
+`python bench.py --gpus N`, which starts that launcher itself before any GPU
+call): one process per GPU.  STRONG scaling: the frame is fixed and split over the ranks
 by libnori_gpu itself (nori_gpu_render_sharded: rank r renders sample passes
 [P r/N, P (r+1)/N), or --shard blocks: every N-th 32x32 block of the spiral
 order), and the library sums the RGBW films into rank 0 with RCCL over xGMI --
@@ -175,6 +176,38 @@ def roofline(ts, samples, config="c2"):
             "ms_per_step_isolated": ts["ms_total"], "kernels": rows}
 
 
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, env, device_count, argv, port=None):
+    """How this invocation runs: None = in this process (one GPU, or this is
+    already rank RANK of a torch.distributed.run job), else the argv of the
+    launcher to run as a child (one process per GPU).  Raises SystemExit on
+    an inconsistent request: --gpus != WORLD_SIZE, or more GPUs than the node
+    has (device_count, counted without initialising HIP)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} < 1")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: pass the launcher's process count")
+        if int(env.get("LOCAL_WORLD_SIZE", world)) > device_count:
+            raise SystemExit(f"bench.py: {env.get('LOCAL_WORLD_SIZE', world)} ranks on this node but only "
+                             f"{device_count} GPU(s) visible")
+        return None
+    if gpus > device_count:
+        raise SystemExit(f"bench.py: --gpus {gpus} but only {device_count} GPU(s) visible")
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port or free_port()}", os.path.abspath(__file__), *argv]
+
+
 def hip_runtime():
     libs = sorted({l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l})
     return libs
@@ -203,6 +236,17 @@ def main():
                          "(the render bench.py's roofline times), then exit")
     args = ap.parse_args()
 
+    # one process per GPU: a plain `bench.py --gpus N` starts the launcher
+    # itself (a child process, before this process touches the GPU) and
+    # exits with its status; torch.cuda.device_count() does not initialise HIP
+    import torch
+
+    plan = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), sys.argv[1:])
+    if plan is not None:
+        import subprocess
+
+        sys.exit(subprocess.run(plan).returncode)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -218,8 +262,6 @@ def main():
         print(json.dumps({"roofline_only": True, "workload": label, "stats": r.last_stats}), flush=True)
         r.close()
         return
-
-    import torch
 
     dist = None
     comm = None
@@ -264,10 +306,18 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     last = r.last_stats
+    rank_ms = [elapsed / args.steps * 1e3]
+    comm_ranks = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t = torch.zeros(world, dtype=torch.float64)
+        t[rank] = elapsed
+        dist.all_reduce(t)  # every rank's time (gloo)
+        rank_ms = [float(x) / args.steps * 1e3 for x in t]
+        elapsed = float(t.max())
+        nr = torch.zeros(world, dtype=torch.int64)
+        nr[rank] = comm.ranks()[0]
+        dist.all_reduce(nr)
+        comm_ranks = nr.tolist()  # the communicator size each rank's library reports
 
     samples_per_step = W * H * spp
     value = samples_per_step * args.steps / elapsed / 1e6
@@ -311,6 +361,8 @@ def main():
             # whole-job ray throughput (all ranks' rays over the step time)
             "grays_per_s": {k: world * last[f"rays_{k}"] / (elapsed / args.steps) / 1e9
                             for k in ("closest", "shadow", "finish")},
+            "per_rank_ms_per_step": rank_ms,
+            "comm_nranks_per_rank": comm_ranks,
             "wavefront_iterations": last["iterations"],
             "stream_parts": last.get("stream_parts", 1),
             "hip_runtime": hip_runtime(),

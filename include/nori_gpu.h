@@ -369,17 +369,28 @@ const char *nori_gpu_comm_library(void);
 #define NORI_SHARD_BLOCKS 1  /* rank r: blocks r, r+N, r+2N, ... of the BlockGenerator's spiral
                                 order (block.cpp:140-188), every pass */
 /* The share of a whole-frame render `desc` that rank `rank` of `nranks`
- * renders: writes this rank's pass range and (BLOCKS) block ids into *out and
+ * renders: writes this rank's pass range and block ids into *out and
  * block_buf (capacity = the frame's block count).  desc->num_blocks != 0
- * restricts the frame to those blocks first.  out->pass_count == 0: the rank
- * has no share (more ranks than passes / blocks).  Pure host function. */
+ * restricts the frame to those blocks first (ids checked against the frame,
+ * duplicates dropped); desc->pass_count == 0 means the scene's sampleCount.
+ * out->pass_count == 0: the rank has no share (more ranks than passes /
+ * blocks).  Pure host function. */
 int nori_gpu_shard_desc(const nori_scene_desc *scene, const nori_gpu_render_desc *desc, int mode, int nranks,
                         int rank, nori_gpu_render_desc *out, uint32_t *block_buf);
 /* Render this rank's share of `desc` into film_dev (device memory on the
  * context's device, (H+2b)x(W+2b)x4 floats; ZEROED first) and sum the films
  * of all ranks on the context's stream: into root's film_dev (ncclReduce), or
  * into every rank's when root < 0 (ncclAllReduce).  Returns after the sum has
- * completed on this rank.  stats: this rank's share. */
+ * completed on this rank.  stats: this rank's share.  desc->variance_out must
+ * be NULL (per-pixel statistics are not summed across ranks).
+ * Failure handling: every rank joins a status exchange before the film sum.
+ * If any rank's share was cancelled (nori_gpu_cancel) every rank returns
+ * NORI_ERR_CANCELLED; if any failed, the failing rank returns its error and
+ * the others NORI_ERR_INVALID ("the frame is incomplete"); no film sum runs.
+ * A HIP error, an RCCL error, or peers that do not reach the collective within
+ * NORI_COMM_TIMEOUT_S seconds (default 600) abort the communicator
+ * (ncclCommAbort) and return NORI_ERR_HIP; an aborted communicator fails every
+ * later call. */
 int nori_gpu_render_sharded(nori_gpu_ctx *ctx, nori_gpu_comm *comm, const nori_gpu_render_desc *desc, int mode,
                             int root, float *film_dev, nori_gpu_stats *stats);
 

@@ -16,9 +16,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "comm.h"
 
@@ -31,6 +33,8 @@ struct RcclApi {
     ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*async_error)(ncclComm_t, ncclResult_t *) = nullptr;
     ncclResult_t (*reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
                            hipStream_t) = nullptr;
     ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
@@ -76,6 +80,8 @@ RcclApi &rccl() {
         api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(sym("ncclGetUniqueId"));
         api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(sym("ncclCommInitRank"));
         api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(sym("ncclCommDestroy"));
+        api.comm_abort = reinterpret_cast<decltype(api.comm_abort)>(sym("ncclCommAbort"));
+        api.async_error = reinterpret_cast<decltype(api.async_error)>(sym("ncclCommGetAsyncError"));
         api.reduce = reinterpret_cast<decltype(api.reduce)>(sym("ncclReduce"));
         api.all_reduce = reinterpret_cast<decltype(api.all_reduce)>(sym("ncclAllReduce"));
         api.error_string = reinterpret_cast<decltype(api.error_string)>(sym("ncclGetErrorString"));
@@ -112,6 +118,54 @@ void *comm_create(const unsigned char *id, int nranks, int rank, int device) {
 
 void comm_destroy(void *c) {
     if (c) (void)rccl().comm_destroy(static_cast<ncclComm_t>(c));
+}
+
+void comm_abort(void *c) {
+    if (c) (void)rccl().comm_abort(static_cast<ncclComm_t>(c));
+}
+
+// hipStreamSynchronize with a watchdog: a peer that died (or never reaches
+// the collective) would leave this rank blocked forever in the RCCL kernel.
+// Poll the stream; an asynchronous RCCL error or `timeout_s` without
+// completion aborts the communicator (ncclCommAbort also releases the kernel
+// waiting on the peer) and throws.
+void comm_wait(void *c, hipStream_t stream, double timeout_s, bool &aborted) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) {
+            comm_abort(c);
+            aborted = true;
+            throw NoriException(NORI_ERR_HIP, std::string("film exchange: ") + hipGetErrorString(e));
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (rccl().async_error(static_cast<ncclComm_t>(c), &ae) == ncclSuccess && ae != ncclSuccess &&
+            ae != ncclInProgress) {
+            comm_abort(c);
+            aborted = true;
+            throw NoriException(NORI_ERR_HIP, std::string("film exchange: RCCL error ") + rccl().error_string(ae));
+        }
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt > timeout_s) {
+            comm_abort(c);
+            aborted = true;
+            throw NoriException(NORI_ERR_HIP, "film exchange: no completion within " + std::to_string(timeout_s) +
+                                                  " s (a peer rank failed or never joined); communicator aborted");
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+int comm_max_int(void *c, int *dev, int *pinned, int value, hipStream_t stream, double timeout_s, bool &aborted) {
+    *pinned = value;
+    if (hipMemcpyAsync(dev, pinned, sizeof(int), hipMemcpyHostToDevice, stream) != hipSuccess)
+        throw NoriException(NORI_ERR_HIP, "status exchange: copy failed");
+    check(rccl().all_reduce(dev, dev, 1, ncclInt32, ncclMax, static_cast<ncclComm_t>(c), stream), "ncclAllReduce");
+    if (hipMemcpyAsync(pinned, dev, sizeof(int), hipMemcpyDeviceToHost, stream) != hipSuccess)
+        throw NoriException(NORI_ERR_HIP, "status exchange: copy failed");
+    comm_wait(c, stream, timeout_s, aborted);
+    return *pinned;
 }
 
 void comm_sum(void *c, float *buf, size_t count, int root, hipStream_t stream) {

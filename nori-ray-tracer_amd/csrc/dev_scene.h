@@ -11,8 +11,9 @@
 // Path queues (two, ping-ponged) hold one path per entry, 52 B + the hit:
 //   ray_o float4 (o.xyz, previous bsdf pdf | -1; a camera ray: 1/z of its
 //                 camera-space direction, so mint = near/z, maxt = far/z)
-//   ray_d float4 (d.xyz, sample record index | bit 31: camera ray; any
-//                 other ray has mint = Epsilon, maxt = inf)
+//   ray_d float4 (d.xyz, sample record index (bits 0-28) | colour channel
+//                 of a chromatic-aberration sample (bits 29-30) | bit 31:
+//                 camera ray; any other ray has mint = Epsilon, maxt = inf)
 //   thr   float4 (beta.rgb, pcg32 state bits 0-31)
 //   rng   uint32 (pcg32 state bits 32-63; the stream increment is
 //                 2 sid + 1 of the sample id, recomputed from the record index)
@@ -78,7 +79,8 @@ struct DevScene {
     int32_t cam_type;          // NORI_CAMERA_*
     float lens_radius, focal;  // thinlens / advancedCamera
     float distortion[2];       // advancedCamera barrel distortion
-    float chromatic[3];        // advancedCamera chromatic aberration (path kernels: zero)
+    float chromatic[3];        // advancedCamera chromatic aberration (zero otherwise)
+    int32_t chroma;            // chromatic != 0: three Li calls per sample, one per colour channel
     int32_t W_max;             // max(W, H)
     float av_length;           // "av" integrator
     float filter[NORI_FILTER_RESOLUTION + 1];
@@ -141,6 +143,8 @@ struct PathQueue {
     uint32_t *rng;   // pcg32 state high word
 };
 constexpr uint32_t kCameraRay = 0x80000000u;  // ray_d.w flag: mint/maxt from the camera clip planes
+constexpr uint32_t kChanShift = 29;            // ray_d.w bits 29-30: colour channel (chromatic aberration)
+constexpr uint32_t kWorkMask = (1u << kChanShift) - 1u;  // record index (work ids < 2^29: runtime chunking)
 
 struct ShadowQueue {
     float4 *ray_o;

@@ -1121,6 +1121,7 @@ struct PathState {
     Pcg rng;
     uint32_t work;
     bool cam;    // the ray is a camera ray (stored with invz instead of prev)
+    uint32_t chan;  // chromatic aberration: the colour channel whose Li this path computes (0 otherwise)
     float invz;  // camera ray: 1/z of its camera-space direction
     V3 L;  // finisher only: the sample's radiance so far (the record, held in registers)
 };
@@ -1143,7 +1144,8 @@ ND void load_path(const DevScene &S, const WorkDesc &wd, const PathQueue &Q, uin
     ps.o = ld3(ro);
     ps.d = ld3(rd);
     const uint32_t wf = __float_as_uint(rd.w);
-    ps.work = wf & ~kCameraRay;
+    ps.work = wf & kWorkMask;
+    ps.chan = (wf >> kChanShift) & 3u;
     ps.cam = (wf & kCameraRay) != 0u;
     ps.invz = ro.w;
     ps.prev = ps.cam ? -1.0f : ro.w;
@@ -1155,7 +1157,8 @@ ND void load_path(const DevScene &S, const WorkDesc &wd, const PathQueue &Q, uin
 }
 ND void store_path(const PathQueue &Q, uint32_t i, const PathState &ps) {
     Q.ray_o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.cam ? ps.invz : ps.prev);
-    Q.ray_d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(ps.work | (ps.cam ? kCameraRay : 0u)));
+    Q.ray_d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z,
+                             __uint_as_float(ps.work | (ps.chan << kChanShift) | (ps.cam ? kCameraRay : 0u)));
     Q.thr[i] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, __uint_as_float((uint32_t)ps.rng.state));
     Q.rng[i] = (uint32_t)(ps.rng.state >> 32);
 }
@@ -1288,6 +1291,17 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
     return r;
 }
 
+// Chromatic aberration (render.cpp:106-121): a sample's value is
+// value0 + value1 + value2 with value_c = e_c * Li_c (e_c the unit colour of
+// channel c), so component c of the record gets Li_c.c and the two other
+// paths add 0 * Li_k.c there -- +-0, or NaN when that term is not finite,
+// which the splat's validity check then drops, as the reference does.  Each
+// contribution of channel c's path goes to the record through this mask.
+ND V3 chan_only(const DevScene &S, uint32_t ch, const V3 &a) {
+    if (!S.chroma) return a;
+    return V3{ch == 0 ? a.x : 0.0f * a.x, ch == 1 ? a.y : 0.0f * a.y, ch == 2 ? a.z : 0.0f * a.z};
+}
+
 #ifndef NORI_SHADE_ATOMIC_REC
 #define NORI_SHADE_ATOMIC_REC 1
 #endif
@@ -1300,7 +1314,8 @@ ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
 // path's bounces are a serial chain, and a record read per bounce would add a
 // memory latency to each.
 template <bool ATOMIC>
-ND void rec_add(float4 *rec, PathState &ps, const V3 &a) {
+ND void rec_add(const DevScene &S, float4 *rec, PathState &ps, const V3 &a0) {
+    const V3 a = chan_only(S, ps.chan, a0);
     if (!ATOMIC) {
         ps.L = ps.L + a;
         return;
@@ -1355,7 +1370,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
         NeeSample ne = nee_sample(S, mp, ps.rng);
         ps.beta = ps.beta * V3{S.albedo[0], S.albedo[1], S.albedo[2]};
         const V3 tr = medium_tr(S, mp, ne.p);
-        so.contrib = ((ps.beta * tr) * ne.Li) * pdf_mat;
+        so.contrib = chan_only(S, ps.chan, ((ps.beta * tr) * ne.Li) * pdf_mat);
         so.emit = !is_zero(so.contrib);
         so.o = mp;
         so.d = ne.wi;
@@ -1384,7 +1399,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
             w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
         }
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
-        rec_add<ATOMIC>(rec, ps, Ladd);
+        rec_add<ATOMIC>(S, rec, ps, Ladd);
     }
     if (skip_nee(S, B, ps.beta)) {
         pcg_skip(ps.rng, 3);
@@ -1400,7 +1415,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
         const float pdf_mat = bsdf_pdf(B, br);
         const float w_ems = (pdf_mat + ne.pdf_em) > 0.0f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
         const V3 tr = medium_tr(S, hs.p, ne.p);
-        so.contrib = ((((ps.beta * w_ems) * f) * theta) * ne.Li) * tr;
+        so.contrib = chan_only(S, ps.chan, ((((ps.beta * w_ems) * f) * theta) * ne.Li) * tr);
         so.emit = !is_zero(so.contrib);
         so.o = hs.p;
         so.d = ne.wi;
@@ -1454,7 +1469,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         } else {
             Ladd = ps.beta * Le;
         }
-        rec_add<ATOMIC>(rec, ps, Ladd);
+        rec_add<ATOMIC>(S, rec, ps, Ladd);
     }
 #ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
@@ -1475,7 +1490,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         V3 f = bsdf_eval(B, br);
         float pdf_mat = bsdf_pdf(B, br);
         float w_ems = (pdf_mat + ne.pdf_em) > 0.0f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
-        so.contrib = (((ps.beta * w_ems) * f) * theta) * ne.Li;
+        so.contrib = chan_only(S, ps.chan, (((ps.beta * w_ems) * f) * theta) * ne.Li);
         so.emit = !is_zero(so.contrib);  // a zero contribution adds nothing (NaN still goes)
         so.o = hs.p;
         so.d = ne.wi;
@@ -1525,10 +1540,29 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t p
     const V2 ap = next2D(ps.rng);  // apertureSample (render.cpp:99)
     camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, -1, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
     ps.cam = true;
+    ps.chan = 0;
     ps.beta = V3{1, 1, 1};
     ps.prev = -1.0f;
     ps.work = w;
     rec[w] = make_float4(0, 0, 0, 0);
+}
+
+// Chromatic aberration: channel ps.chan's Li has ended, so the sample goes on
+// with the next channel's camera ray (render.cpp:106-121: the three rays share
+// the pixel and aperture samples, their Li calls consume the sampler in turn,
+// so the pcg32 state simply continues).
+ND void next_channel(const DevScene &S, const WorkDesc &wd, PathState &ps) {
+    const uint32_t pass = ps.work / wd.M, pix = wd.pixels[ps.work - pass * wd.M];
+    const uint32_t W = (uint32_t)S.W, y = pix / W, x = pix - y * W;
+    Pcg r;
+    wave_seed(r, wd.seed, (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + pix);
+    const V2 jit = next2D(r);
+    const V2 ap = next2D(r);
+    ps.chan += 1;
+    camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, (int)ps.chan, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
+    ps.cam = true;
+    ps.beta = V3{1, 1, 1};
+    ps.prev = -1.0f;
 }
 
 // Closest hit of a path's ray (scan mode, TRACE builds of k_shade).
@@ -1611,7 +1645,14 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     __builtin_amdgcn_s_waitcnt(0);  // path loads landed: phase 1 is the shading proper
     NORI_SPHASE(0)
 #endif
-    if (tid < n_in) alive = shade_vertex<INTEG, true>(S, ps, hit, rec, so);
+    if (tid < n_in) {
+        alive = shade_vertex<INTEG, true>(S, ps, hit, rec, so);
+        ps.cam = false;  // a survivor carries its BSDF-sampled ray (Epsilon, inf)
+        if (!alive && S.chroma && ps.chan < 2) {  // the sample's next colour channel
+            next_channel(Sg, wd, ps);
+            alive = true;
+        }
+    }
     NORI_SPHASE(1)
     s_w[tid] = wspec < wd.total ? (uint32_t)wspec : ~0u;
     s_pix[tid] = pspec;
@@ -1660,7 +1701,6 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         sq.payload[i] = make_float4(so.contrib.x, so.contrib.y, so.contrib.z, __uint_as_float(so.work));
     }
     if (TRACE && alive) trace_into(Sg, ps, out.hit + b * kSeg + al_off);
-    ps.cam = false;  // a survivor carries its BSDF-sampled ray (Epsilon, inf)
     if (alive) store_path(out, b * kSeg + al_off, ps);
     NORI_SPHASE(3)
     // ---- regeneration: the free slots [al_tot, kSeg) take the next work ids of
@@ -1756,7 +1796,7 @@ ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, ui
 __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg, int sel, float4 *rec) {
     const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
     if (idx >= seg.cnt[sel][sg]) return;
-    rec[__float_as_uint(Q.ray_d[sg * kSeg + idx].w) & ~kCameraRay].w = 1.0f;
+    rec[__float_as_uint(Q.ray_d[sg * kSeg + idx].w) & kWorkMask].w = 1.0f;
 }
 
 // Cooperative scan (scan-mode scenes, n <= 64 primitives): the rays of the
@@ -1978,6 +2018,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             if (so.emit && !occluded) ps.L = ps.L + so.contrib;  // so.work == ps.work
         }
         NORI_PHASE(1)
+        if (active && !alive && S.chroma && ps.chan < 2) {  // the sample's next colour channel
+            next_channel(Sg, wd, ps);
+            alive = true;
+        }
         if (active && !alive) {
             active = false;
             // the sample is complete: splat it (k_splat skipped it as pending)

@@ -238,7 +238,13 @@ struct nori_gpu_ctx {
 struct nori_gpu_comm {
     void *nccl = nullptr;  // ncclComm_t (comm.cpp)
     int nranks = 1, rank = 0, device = 0;
-    ~nori_gpu_comm() { comm_destroy(nccl); }
+    bool aborted = false;   // ncclCommAbort ran: every later call fails
+    int *status_dev = nullptr, *status_host = nullptr;  // the per-render status exchange word
+    ~nori_gpu_comm() {
+        if (!aborted) comm_destroy(nccl);
+        if (status_dev) (void)hipFree(status_dev);
+        if (status_host) (void)hipHostFree(status_host);
+    }
 };
 
 namespace {
@@ -618,6 +624,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.distortion[0] = cam.distortion[0];
     S.distortion[1] = cam.distortion[1];
     for (int k = 0; k < 3; ++k) S.chromatic[k] = cam.camera_type == NORI_CAMERA_ADVANCED ? cam.chromatic[k] : 0.0f;
+    S.chroma = S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f;
     S.W_max = cam.width > cam.height ? cam.width : cam.height;
     S.av_length = d.av_length;
     filter_table(cam, S.filter);
@@ -844,7 +851,9 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
     const uint32_t M = (uint32_t)pixels.size(), passes = rd.pass_count;
     const size_t rec_budget = (size_t)4 << 30;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(passes, rec_budget / (16 * (size_t)M)));
-    chunk = (uint32_t)std::min<uint64_t>(chunk, ((uint64_t)1 << 31) / M);
+    // work ids (record indices) < 2^29: the path queue keeps a chromatic
+    // sample's colour channel in bits 29-30 of the same word (kWorkMask)
+    chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, ((uint64_t)1 << kChanShift) / M));
     c.rec.ensure(16 * (size_t)chunk * M);
     c.counters.ensure(sizeof(Counters));
     const size_t film_elems = 4 * (size_t)(W + 2 * B) * (H + 2 * B);
@@ -977,9 +986,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     const uint32_t passes = rd.pass_count ? rd.pass_count : 0;
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
     const bool one_bounce = S.integrator >= NORI_INTEGRATOR_NORMALS;
-    if (!one_bounce && (S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f))
-        throw NoriException(NORI_ERR_UNSUPPORTED,
-                            "chromatic aberration (three rays per sample) is on the one-bounce integrators only");
     // default pool: about 1/16 of the render's samples in flight, between 1M
     // and 4M paths (~0.9 GB of queues at 4M).  Large pools hide the shade
     // kernel's memory latency (4M measured best among 256K..4M on cbox at 512
@@ -987,6 +993,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // spend less time draining a smaller pool (cbox 64 spp: 4M 2190, 2M 2320,
     // 1M 2400 Msamples/s; 512 spp: 4M and 2M within 1 %).
     if (one_bounce) return render_one_bounce(c, rd, pixels, blocks, rgbw_out, stats, t0);
+    if (M > kWorkMask) throw NoriException(NORI_ERR_INVALID, "frame too large: more than 2^29 pixels per pass");
     uint32_t pool = rd.path_pool;
     if (!pool) {  // NORI_PATH_POOL: default pool size override (tuning)
         const char *e = std::getenv("NORI_PATH_POOL");
@@ -1003,7 +1010,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // sample-record budget: chunks of passes, each < 2^31 records
     const size_t rec_budget = (size_t)6 << 30;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(passes, rec_budget / (16 * (size_t)M)));
-    chunk = (uint32_t)std::min<uint64_t>(chunk, ((uint64_t)1 << 31) / M);
+    // work ids (record indices) < 2^29: the path queue keeps a chromatic
+    // sample's colour channel in bits 29-30 of the same word (kWorkMask)
+    chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, ((uint64_t)1 << kChanShift) / M));
     c.rec.ensure(16 * (size_t)chunk * M);
     c.counters.ensure(sizeof(Counters));
     const size_t film_elems = 4 * (size_t)(W + 2 * B) * (H + 2 * B);
@@ -1277,26 +1286,34 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
 // ------------------------------------------------------------------ C ABI
 namespace {
 
-// This rank's share of a whole-frame render (nori_gpu_shard_desc).
+// This rank's share of a whole-frame render (nori_gpu_shard_desc).  The pass
+// count defaults to the scene's sampleCount (0 -> 1) in both entry points, and
+// a block list is checked (range) and de-duplicated in both modes, so the
+// share always fits the caller's block_buf (capacity = the frame's blocks).
 nori_gpu_render_desc shard_of(int W, int H, uint32_t spp, const nori_gpu_render_desc &whole, int mode, int nranks,
                               int rank, std::vector<uint32_t> &blocks) {
     if (nranks < 1 || rank < 0 || rank >= nranks) throw NoriException(NORI_ERR_INVALID, "shard: rank out of range");
     if (mode != NORI_SHARD_PASSES && mode != NORI_SHARD_BLOCKS) throw NoriException(NORI_ERR_INVALID, "shard: unknown mode");
     nori_gpu_render_desc out = whole;
-    const uint32_t P = whole.pass_count ? whole.pass_count : spp;
+    const uint32_t P = whole.pass_count ? whole.pass_count : std::max<uint32_t>(spp, 1u);
+    const uint32_t nb = (uint32_t)(((W + NORI_BLOCK_SIZE - 1) / NORI_BLOCK_SIZE) * ((H + NORI_BLOCK_SIZE - 1) / NORI_BLOCK_SIZE));
+    std::vector<char> want(nb, whole.num_blocks ? 0 : 1);
+    for (uint32_t i = 0; i < whole.num_blocks; ++i) {
+        if (whole.block_ids[i] >= nb) throw NoriException(NORI_ERR_INVALID, "block id out of range");
+        want[whole.block_ids[i]] = 1;
+    }
     blocks.clear();
     if (mode == NORI_SHARD_PASSES) {
         const uint64_t a = (uint64_t)P * rank / nranks, b = (uint64_t)P * (rank + 1) / nranks;
         out.pass_begin = whole.pass_begin + (uint32_t)a;
         out.pass_count = (uint32_t)(b - a);
-        if (whole.num_blocks) blocks.assign(whole.block_ids, whole.block_ids + whole.num_blocks);
+        if (whole.num_blocks)  // the restricted frame, each block once, in the caller's order
+            for (uint32_t i = 0; i < whole.num_blocks; ++i)
+                if (want[whole.block_ids[i]]) {
+                    blocks.push_back(whole.block_ids[i]);
+                    want[whole.block_ids[i]] = 0;
+                }
     } else {
-        const uint32_t nb = (uint32_t)(std::ceil(W / (float)NORI_BLOCK_SIZE) * std::ceil(H / (float)NORI_BLOCK_SIZE));
-        std::vector<char> want(nb, whole.num_blocks ? 0 : 1);
-        for (uint32_t i = 0; i < whole.num_blocks; ++i) {
-            if (whole.block_ids[i] >= nb) throw NoriException(NORI_ERR_INVALID, "block id out of range");
-            want[whole.block_ids[i]] = 1;
-        }
         uint32_t k = 0;  // round-robin over the spiral order (block.cpp:140-188)
         for (uint32_t b : spiral_blocks(W, H))
             if (want[b] && (k++ % (uint32_t)nranks) == (uint32_t)rank) blocks.push_back(b);
@@ -1305,6 +1322,14 @@ nori_gpu_render_desc shard_of(int W, int H, uint32_t spp, const nori_gpu_render_
     out.num_blocks = (uint32_t)blocks.size();
     out.block_ids = blocks.empty() ? nullptr : blocks.data();
     return out;
+}
+
+// Watchdog of the film exchange (NORI_COMM_TIMEOUT_S, default 600 s): how long
+// a rank waits for its peers in a collective before aborting the communicator.
+double comm_timeout_s() {
+    const char *e = std::getenv("NORI_COMM_TIMEOUT_S");
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0.0 ? v : 600.0;
 }
 
 }  // namespace
@@ -1536,22 +1561,60 @@ int nori_gpu_render_sharded(nori_gpu_ctx *c, nori_gpu_comm *comm, const nori_gpu
     return guarded([&] {
         if (!c || !comm || !rd || !film) return fail(NORI_ERR_INVALID, "null argument");
         if (rd->num_blocks && !rd->block_ids) return fail(NORI_ERR_INVALID, "block_ids is null");
+        if (rd->variance_out)  // per-pixel statistics are not summed across ranks
+            return fail(NORI_ERR_INVALID, "nori_gpu_render_sharded: variance_out must be NULL");
         if (root >= comm->nranks) return fail(NORI_ERR_INVALID, "root out of range");
         if (comm->device != c->device) return fail(NORI_ERR_INVALID, "communicator and context on different devices");
+        if (comm->aborted) return fail(NORI_ERR_HIP, "communicator was aborted by an earlier failure");
         HIP_TRY(hipSetDevice(c->device));
         std::vector<uint32_t> blocks;
         nori_gpu_render_desc s = shard_of(c->S.W, c->S.H, c->spp, *rd, mode, comm->nranks, comm->rank, blocks);
         s.output_on_device = 1;
+        s.variance_out = nullptr;
         const size_t n = 4 * (size_t)(c->S.W + 2 * c->S.border) * (size_t)(c->S.H + 2 * c->S.border);
         HIP_TRY(hipMemsetAsync(film, 0, n * sizeof(float), c->stream));
+        // This rank's share.  A failure or a cancel (nori_gpu_cancel) must not
+        // leave the peers blocked in the film sum: every rank joins a status
+        // exchange first (max over ranks of severity << 16 | rank), and the
+        // film sum runs only if every rank rendered its share.
         int rc = NORI_OK;
-        if (s.pass_count)
-            rc = render(*c, s, film, stats);
-        else if (stats)
+        std::string err;
+        if (s.pass_count) {
+            try {
+                rc = render(*c, s, film, stats);
+            } catch (const NoriException &e) {
+                rc = e.code;
+                err = e.what();
+            } catch (const std::bad_alloc &) {
+                rc = NORI_ERR_OOM;
+                err = "out of memory";
+            }
+            if (rc != NORI_OK && err.empty()) err = g_last_error;
+        } else if (stats) {
             std::memset(stats, 0, sizeof(*stats));
-        if (rc != NORI_OK) return rc;  // (a failed rank leaves the others waiting in the sum: as any collective)
+        }
+        const double timeout = comm_timeout_s();
+        if (rc == NORI_ERR_HIP) {
+            // the device or its stream may be unusable: abort, so the peers'
+            // status exchange fails (they see the abort or time out) instead of hanging
+            comm_abort(comm->nccl);
+            comm->aborted = true;
+            return fail(rc, err);
+        }
+        if (!comm->status_dev) {
+            HIP_TRY(hipMalloc((void **)&comm->status_dev, sizeof(int)));
+            HIP_TRY(hipHostMalloc((void **)&comm->status_host, sizeof(int), hipHostMallocDefault));
+        }
+        const int sev = rc == NORI_OK ? 0 : (rc == NORI_ERR_CANCELLED ? 1 : 2);
+        const int all = comm_max_int(comm->nccl, comm->status_dev, comm->status_host, (sev << 16) | comm->rank,
+                                     c->stream, timeout, comm->aborted);
+        if (rc != NORI_OK) return fail(rc, err);
+        if ((all >> 16) != 0)
+            return fail((all >> 16) == 1 ? NORI_ERR_CANCELLED : NORI_ERR_INVALID,
+                        "the frame is incomplete: rank " + std::to_string(all & 0xFFFF) +
+                            ((all >> 16) == 1 ? " was cancelled" : " failed to render its share"));
         comm_sum(comm->nccl, film, n, root, c->stream);
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        comm_wait(comm->nccl, c->stream, timeout, comm->aborted);
         return (int)NORI_OK;
     });
 }

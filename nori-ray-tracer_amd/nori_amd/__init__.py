@@ -295,11 +295,16 @@ class GpuRenderer:
         return rd, ids
 
     def render_sharded(self, comm, device_ptr, passes=None, pass_begin=0, blocks=None, mode="passes", root=0,
-                       seed=0, path_pool=0, timing=False):
+                       seed=0, path_pool=0, timing=False, variance=None):
         """This rank's share of the frame into the device film at `device_ptr`
         (zeroed first), then the RCCL sum of every rank's film into root's
-        (root=-1: into every rank's) -- nori_gpu_render_sharded."""
+        (root=-1: into every rank's) -- nori_gpu_render_sharded.  A cancel or
+        failure on any rank raises NoriError on every rank (no rank hangs in
+        the sum).  `variance` must stay None: the library rejects per-pixel
+        statistics for sharded renders (they are not summed across ranks)."""
         rd, ids = self._desc(passes, pass_begin, blocks, seed, path_pool, timing)
+        if variance is not None:
+            rd.variance_out = int(variance)
         st = _abi.Stats()
         check(lib().nori_gpu_render_sharded(self._h, comm.handle, C.byref(rd), _abi.SHARD_MODES[mode], int(root),
                                             C.c_void_p(int(device_ptr)), C.byref(st)))

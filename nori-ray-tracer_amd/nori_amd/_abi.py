@@ -1,4 +1,4 @@
-"""ctypes mirror of include/nori_gpu.h (ABI version 4).
+"""ctypes mirror of include/nori_gpu.h (ABI version 5, _abi.ABI_VERSION).
 
 The structures below must match the C declarations field for field; the
 test suite checks their sizes against the library (tests/test_abi.py).

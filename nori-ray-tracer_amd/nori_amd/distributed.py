@@ -44,6 +44,12 @@ class FilmComm:
         check(lib().nori_gpu_comm_create(buf, int(nranks), int(rank), int(device), C.byref(h)))
         self.handle, self.nranks, self.rank, self.device = h, nranks, rank, device
 
+    def ranks(self):
+        """(nranks, rank) as the library's communicator reports them (nori_gpu_comm_rank)."""
+        n, r = C.c_int(), C.c_int()
+        check(lib().nori_gpu_comm_rank(self.handle, C.byref(n), C.byref(r)))
+        return n.value, r.value
+
     def close(self):
         if self.handle is not None and self.handle.value:
             lib().nori_gpu_comm_destroy(self.handle)

@@ -159,3 +159,33 @@ def compare_to_png(img, ref_lin, block=50, scale=1.0):
     ratio = img.reshape(-1, 3).mean(0) / np.maximum(ref_lin.reshape(-1, 3).mean(0), 1e-12)
     return {"mean_ratio": ratio, "rel_median": float(np.median(rel)), "rel_p95": float(np.percentile(rel, 95)),
             "rel_max": float(rel.max())}
+
+
+# Image parity against the oracle on identical WAVE streams (tests/test_gpu_*.py).
+# BASELINE.json's bar is per-pixel L2 < 1e-3; the tests assert what the code
+# achieves.  Transcendentals differ by a few ulp between the ROCm device
+# library and glibc, which can flip a rare branch: one flipped sample moves one
+# pixel, so up to 0.01 % of the pixels (at least one) are left out of the
+# trimmed L2; the film sums arrive in a different order on the two sides.
+L2_TOL = 1e-7           # whole-image L2 (one flipped sample of an 80x60 frame stays under it)
+L2_TRIMMED_TOL = 1e-9   # L2 without the worst 0.01 % of the pixels
+# pixels whose three channels agree to 1e-3 relative (1e-5 absolute): a few-ulp
+# direction difference grows along a long glass-sphere path (chaotic), so
+# paths that stay inside the sphere for a hundred bounces may end a little
+# apart (measured 99.4 % of the pixels within 1e-4 on 64x48 cbox path_mis)
+PIXEL_MATCH = 0.99
+
+
+def image_parity(gpu, cpu):
+    """L2, trimmed L2 and matching-pixel fraction of two (H, W, 3) images."""
+    d = np.mean((np.asarray(gpu, np.float64) - np.asarray(cpu, np.float64)) ** 2, axis=-1).ravel()
+    k = max(1, int(d.size * 1e-4))
+    trimmed = float(np.sort(d)[:-k].mean()) if d.size > k else 0.0
+    match = float(np.mean(np.all(np.isclose(gpu, cpu, rtol=1e-3, atol=1e-5), axis=-1)))
+    return {"l2": float(d.mean()), "l2_trimmed": trimmed, "pixel_match": match}
+
+
+def assert_parity(p, l2_tol=L2_TOL):
+    assert p["l2"] < l2_tol, p
+    assert p["l2_trimmed"] < L2_TRIMMED_TOL, p
+    assert p["pixel_match"] >= PIXEL_MATCH, p

@@ -6,8 +6,13 @@ Tolerances:
   equal except where two primitives return the identical t (shared edges),
   where the reference's DFS order picks the last one visited.
 * images: same WAVE random streams on both sides; transcendentals differ by a
-  few ulp (ROCm device library vs glibc), which flips rare branches, so the
-  bar is per-pixel L2 < 1e-3 on linear RGB (BASELINE.json north_star).
+  few ulp (ROCm device library vs glibc), which can flip a rare branch, and the
+  film sums arrive in another order.  BASELINE.json's bar is per-pixel L2 <
+  1e-3 on linear RGB; the tests assert what the code achieves (measured 1e-15
+  to 3e-12 at these sizes, nori_test_util.image_parity): L2 <= 1e-7 -- one
+  flipped sample in an 80x60 frame stays under it, a BSDF lobe biased by 1 % on
+  cbox (mean ~0.13) does not -- L2 <= 1e-9 without the worst 0.01 % of the
+  pixels, and >= 99 % of the pixels equal to 1e-3 relative.
 """
 import os
 
@@ -19,12 +24,9 @@ import synth
 import nori_amd
 import pyoracle
 from conftest import scene_path
-from nori_test_util import load_test_scenes, parse_test_xml, students_t_test
+from nori_test_util import L2_TOL, assert_parity, image_parity, load_test_scenes, parse_test_xml, students_t_test
 
 pytestmark = pytest.mark.gpu
-
-L2_TOL = 1e-3
-
 
 def _rays(n, seed, lo, hi, mint=1e-4, axis_aligned=0.1):
     rng = np.random.default_rng(seed)
@@ -110,8 +112,9 @@ def test_render_scene_matches_oracle(built, parts):
     assert np.isfinite(gpu).all()
     l2 = float(np.mean((gpu - cpu) ** 2))
     exact = float(np.mean(np.all(raw == cpu_raw, axis=-1)))
-    print(f"{'/'.join(parts)}: L2 {l2:.3e}, bit-identical film cells {exact:.3f}")
-    assert l2 < L2_TOL
+    p = image_parity(gpu, cpu)
+    print(f"{'/'.join(parts)}: {p}, bit-identical film cells {exact:.3f}")
+    assert_parity(p)
     assert float(np.mean(gpu)) > 0.0
 
 
@@ -123,11 +126,12 @@ def test_render_envmap_matches_oracle(built, tmp_path, integrator):
     with nori_amd.GpuRenderer(s, 0) as r:
         raw = r.render()
     gpu = nori_amd.develop(s, raw)
-    cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
+    cpu_raw = pyoracle.OracleScene(s).render(rng="wave")
+    cpu = nori_amd.develop(s, cpu_raw)
     assert np.isfinite(gpu).all()
-    l2 = float(np.mean((gpu - cpu) ** 2))
-    print(f"envmap {integrator}: L2 {l2:.3e} mean {gpu.mean():.4f}")
-    assert l2 < L2_TOL
+    p = image_parity(gpu, cpu)
+    print(f"envmap {integrator}: {p}, mean {gpu.mean():.4f}")
+    assert_parity(p)
     assert float(gpu.mean()) > 0.05  # the sky lights the box through its open side
 
 
@@ -135,15 +139,17 @@ def test_render_envmap_matches_oracle(built, tmp_path, integrator):
 def test_render_matches_oracle(built, xml):
     s = nori_amd.load_scene(scene_path("pa4", "cbox", xml), 96, 72, 16)
     with nori_amd.GpuRenderer(s, 0) as r:
-        gpu = nori_amd.develop(s, r.render())
+        raw = r.render()
+        gpu = nori_amd.develop(s, raw)
         st = r.last_stats
-    cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
+    cpu_raw = pyoracle.OracleScene(s).render(rng="wave")
+    cpu = nori_amd.develop(s, cpu_raw)
     assert st["samples"] == 96 * 72 * 16
     assert np.isfinite(gpu).all()
-    l2 = float(np.mean((gpu - cpu) ** 2))
     rel = float(np.mean((gpu - cpu) ** 2 / (cpu ** 2 + 1e-2)))
-    print(f"{xml}: L2 {l2:.3e} relMSE {rel:.3e}")
-    assert l2 < L2_TOL
+    p = image_parity(gpu, cpu)
+    print(f"{xml}: {p}, relMSE {rel:.3e}")
+    assert_parity(p)
 
 
 def test_render_pass_split_and_pool_invariance(cbox):
@@ -190,10 +196,10 @@ def test_render_large_mesh_matches_oracle(hfield):
     s, r, o = hfield
     gpu = nori_amd.develop(s, r.render())
     cpu = nori_amd.develop(s, o.render(rng="wave"))
-    l2 = float(np.mean((gpu - cpu) ** 2))
-    print(f"heightfield microfacet path_mis: L2 {l2:.3e}")
+    p = image_parity(gpu, cpu)
+    print(f"heightfield microfacet path_mis: {p}")
     assert np.isfinite(gpu).all()
-    assert l2 < L2_TOL
+    assert_parity(p)
 
 
 @pytest.mark.parametrize("mode", ["scan", "bvh"])
@@ -203,4 +209,4 @@ def test_render_modes_agree(built, mode):
     gpu = nori_amd.develop(s, r.render())
     r.close()
     cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
-    assert float(np.mean((gpu - cpu) ** 2)) < L2_TOL
+    assert_parity(image_parity(gpu, cpu))

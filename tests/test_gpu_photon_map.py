@@ -5,8 +5,9 @@ search over the same photons).
 Both sides trace photon e from the stream wave_seed(kPhotonSeed, e)
 (deviation D8) and keep the first photonCount stored photons in emission
 order, quantized through PhotonData; the camera paths use the WAVE streams.
-Tolerance: per-pixel L2 < 1e-3 on linear RGB (BASELINE.json north_star); the
-only expected difference is the summation order of the gathered photons.
+Tolerance: per-pixel L2 <= 1e-7 on linear RGB (BASELINE.json's bar is 1e-3;
+measured <= 8e-9); the only expected difference is the summation order of the
+gathered photons.
 """
 import time
 
@@ -19,7 +20,7 @@ from test_photon_map import pmap_scene
 
 pytestmark = pytest.mark.gpu
 
-L2_TOL = 1e-3
+L2_TOL = 1e-7
 
 
 def _compare(s):

@@ -8,13 +8,17 @@ random streams from the PNG's), compared in linear space: channel means
 within 0.3 %, 50x50-block means within 1 % (median) / 3 % (p95).
 
 Headline size: cbox_path_mis at 512x512, 32 spp, identical WAVE streams on
-both sides: per-pixel L2 < 1e-3 (BASELINE.json north_star).
+both sides (nori_test_util.image_parity): L2 <= 1e-5 -- 8.4M samples, so a
+few flipped branches (a caustic sample through the glass sphere moves its
+pixel by ~0.5) are expected; measured 1e-9 to 2.3e-7 -- and L2 <= 1e-9 without
+the worst 0.01 % of the pixels, >= 99 % of the pixels equal to 1e-3
+relative (BASELINE.json's bar is L2 < 1e-3).
 
 C3 size: the synthetic 524,288-triangle height field (BASELINE config 3's
 ajax.obj is missing from the reference checkout): hit distance bit-exact and
 primitive id equal on >99.9 % of 35k rays (deep BVH: the LDS short stack
 spills to private memory), shadow-ray occlusion identical, and a 64x64 @ 4 spp
-microfacet path_mis image at L2 < 1e-3.
+microfacet path_mis image at L2 <= 1e-7.
 """
 import os
 
@@ -26,6 +30,7 @@ import pyoracle
 import synth
 from conftest import ROOT, scene_path
 from nori_test_util import REFERENCE_PNG_PAIRS, compare_to_png, png_linear
+from nori_test_util import assert_parity, image_parity
 from test_gpu_parity import _compare_hits, _rays
 
 pytestmark = pytest.mark.gpu
@@ -54,10 +59,10 @@ def test_headline_size_matches_oracle(built):
         st = r.last_stats
     cpu_raw = pyoracle.OracleScene(s).render(rng="wave")
     gpu, cpu = nori_amd.develop(s, raw), nori_amd.develop(s, cpu_raw)
-    l2 = float(np.mean((gpu - cpu) ** 2))
-    print(f"cbox_path_mis 512x512@32: L2 {l2:.3e}, invalid {st['invalid_samples']}")
+    p = image_parity(gpu, cpu)
+    print(f"cbox_path_mis 512x512@32: {p}, invalid {st['invalid_samples']}")
     assert st["samples"] == 512 * 512 * 32
-    assert l2 < 1e-3
+    assert_parity(p, l2_tol=1e-5)
 
 
 @pytest.fixture(scope="module")
@@ -85,7 +90,7 @@ def test_c3_size_render_matches_oracle(c3):
     s, r, o = c3
     gpu = nori_amd.develop(s, r.render())
     cpu = nori_amd.develop(s, o.render(rng="wave"))
-    l2 = float(np.mean((gpu - cpu) ** 2))
-    print(f"C3 524k-triangle height field, microfacet path_mis 64x64@4: L2 {l2:.3e}")
+    p = image_parity(gpu, cpu)
+    print(f"C3 524k-triangle height field, microfacet path_mis 64x64@4: {p}")
     assert np.isfinite(gpu).all()
-    assert l2 < 1e-3
+    assert_parity(p)

@@ -75,3 +75,54 @@ def test_render_sharded_one_rank(built, mode):
         torch.cuda.synchronize()
     comm.close()
     assert np.allclose(film.cpu().numpy(), host, rtol=1e-4, atol=1e-4)
+
+
+def test_render_sharded_rejects_variance(built):
+    """Per-pixel statistics are not summed across ranks: a sharded render
+    with variance_out set fails with NORI_ERR_INVALID before touching it."""
+    s = _scene("cbox_path_mis.xml", 32, 32, 2)
+    comm = nd.FilmComm(nd.comm_id(), 1, 0, 0)
+    with nori_amd.GpuRenderer(s, 0) as r:
+        film = torch.zeros(s.film_shape(), dtype=torch.float32, device="cuda:0")
+        host_stats = np.zeros((s.height, s.width, 8), np.float32)
+        with pytest.raises(nori_amd.NoriError) as e:
+            r.render_sharded(comm, film.data_ptr(), variance=host_stats.ctypes.data)
+        assert e.value.code == nori_amd._abi.NORI_ERR_INVALID
+        r.render_sharded(comm, film.data_ptr())  # the communicator still works
+        torch.cuda.synchronize()
+    comm.close()
+
+
+def test_render_sharded_cancel_returns_and_comm_survives(built):
+    """nori_gpu_cancel during a sharded render: the rank still joins the status
+    exchange (no hang), returns NORI_ERR_CANCELLED, and the communicator stays
+    usable for the next frame."""
+    import threading
+    import time
+
+    s = _scene("cbox_path_mis.xml", 2048, 2048, 512)
+    comm = nd.FilmComm(nd.comm_id(), 1, 0, 0)
+    with nori_amd.GpuRenderer(s, 0) as r:
+        film = torch.zeros(s.film_shape(), dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()
+        err = []
+
+        def run():
+            try:
+                r.render_sharded(comm, film.data_ptr())
+            except nori_amd.NoriError as e:
+                err.append(e)
+
+        th = threading.Thread(target=run)
+        t0 = time.time()
+        th.start()
+        time.sleep(0.15)
+        r.cancel()
+        th.join(timeout=60)
+        assert not th.is_alive()
+        assert err and err[0].code == nori_amd._abi.NORI_ERR_CANCELLED, err
+        assert time.time() - t0 < 30
+        r.render_sharded(comm, film.data_ptr(), passes=2)
+        torch.cuda.synchronize()
+        assert r.last_stats["samples"] == 2048 * 2048 * 2
+    comm.close()

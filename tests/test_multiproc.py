@@ -87,3 +87,23 @@ def test_shard_partitions_the_frame(built):
     got = sorted(b for r in range(2) for b in nd.shard(scene, r, 2, "blocks", blocks=sub)[2])
     assert got == sub
     assert nd.shard(scene, 1, 2, "passes", passes=4, pass_begin=10)[:2] == (12, 2)
+
+
+def test_shard_block_lists_are_checked_and_deduplicated(built):
+    """Both modes check a restricting block list against the frame and drop
+    repeated ids, so a share never overflows the caller's block buffer (one
+    entry per frame block); the pass count defaults to the scene's spp."""
+    import nori_amd
+    from nori_amd import distributed as nd
+
+    scene = nori_amd.load_scene(SCENE, W, H, SPP)
+    nb = scene.num_blocks()
+    dup = [1, 4, 1, 4, 4, 0] * 3
+    pb, pc, blocks = nd.shard(scene, 0, 2, "passes", blocks=dup)
+    assert (pb, pc) == (0, SPP // 2) and blocks == [1, 4, 0]
+    got = sorted(b for r in range(3) for b in nd.shard(scene, r, 3, "blocks", blocks=dup)[2])
+    assert got == [0, 1, 4]
+    for mode in ("passes", "blocks"):
+        with pytest.raises(nori_amd.NoriError):
+            nd.shard(scene, 0, 2, mode, blocks=[0, nb])
+    assert nd.shard(scene, 1, 2, "passes", passes=0)[:2] == (SPP // 2, SPP - SPP // 2)
