@@ -34,6 +34,11 @@ struct DevShape {
     float center[3], radius;
     float area_norm;     // DiscretePDF::getNormalization (mesh) or sphere pdf
     int32_t nm_w, nm_h, nm_wrap;  // NormalMap (meshes with normals, mesh.cpp:147-155)
+    // sphere only: no other primitive meets the closed ball (host-checked with
+    // a margin, and the ball lies inside the scene box): a ray from a point of
+    // this sphere that hits it again hits nothing before (the chord is inside
+    // the ball), so the tail finisher takes that hit without a scene scan
+    int32_t solitary;
     const uint32_t *nmap;         // RGBX8 texels in global memory, or null
 };
 
@@ -81,6 +86,10 @@ struct DevScene {
     float distortion[2];       // advancedCamera barrel distortion
     float chromatic[3];        // advancedCamera chromatic aberration (zero otherwise)
     int32_t chroma;            // chromatic != 0: three Li calls per sample, one per colour channel
+    // 1: only the basic plugins (constant-albedo diffuse, mirror, dielectric;
+    // area lights; perspective camera; no normal maps): the path kernels run
+    // their FULL = false variants (device_math.h albedo_at)
+    int32_t basic;
     int32_t W_max;             // max(W, H)
     float av_length;           // "av" integrator
     float filter[NORI_FILTER_RESOLUTION + 1];

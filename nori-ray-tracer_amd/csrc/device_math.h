@@ -267,7 +267,15 @@ struct BRec {
 
 // Texture<Color3f>::eval: constant (consttexture.cpp), Checkerboard::eval
 // (checkerboard.cpp:22-27) or ImageTexture::eval (imagetexture.cpp:118-134)
+// FULL = false: the "basic" plugin set of the path kernels' lite variants
+// (scenes with constant-albedo diffuse, mirror and dielectric BSDFs only,
+// area lights, the perspective camera; runtime.hip basic_scene): the code of
+// the other plugins is not compiled in, so the kernels stay small (their
+// instruction working set fits the instruction cache, which the lone-lane
+// tail paths of k_finish are bound by).
+template <bool FULL = true>
 ND V3 albedo_at(const DevBsdf &b, V2 uv) {
+    if (!FULL) return V3{b.albedo[0], b.albedo[1], b.albedo[2]};
     if (b.tex == NORI_TEXTURE_IMAGE) return texel_rgb(texel_at(b.img, b.img_w, b.img_h, b.img_wrap, uv));
     if (b.tex != NORI_TEXTURE_CHECKERBOARD) return V3{b.albedo[0], b.albedo[1], b.albedo[2]};
     const int x = (int)fabsf(floorf(uv.x / b.tex_scale[0] - b.tex_delta[0]));
@@ -299,12 +307,14 @@ ND float ggx(float NdotV, float alphaG) {  // disney.cpp:31-36
 }
 ND V3 lerp3(float t, V3 a, V3 c) { return a * (1.0f - t) + c * t; }  // disney.cpp:40-42
 
+template <bool FULL = true>
 ND V3 bsdf_eval(const DevBsdf &b, const BRec &r) {
     switch (b.type) {
     case NORI_BSDF_DIFFUSE:  // diffuse.cpp:72-82
         if (r.measure != kMeasureSolidAngle || r.wi.z <= 0 || r.wo.z <= 0) return V3{0, 0, 0};
-        return albedo_at(b, r.uv) * kInvPi;
+        return albedo_at<FULL>(b, r.uv) * kInvPi;
     case NORI_BSDF_MICROFACET: {  // microfacet.cpp:79-90
+        if constexpr (!FULL) return V3{0, 0, 0};
         V3 n = normalize(r.wi + r.wo);
         float D = beckmann_D(b, n);
         float F = fresnel(dot(n, r.wi), b.ext_ior, b.int_ior);
@@ -315,6 +325,7 @@ ND V3 bsdf_eval(const DevBsdf &b, const BRec &r) {
         return V3{d.x + spec, d.y + spec, d.z + spec};
     }
     case NORI_BSDF_DISNEY: {  // disney.cpp:63-114
+        if constexpr (!FULL) return V3{0, 0, 0};
         float NdotV = r.wi.z, NdotL = r.wo.z;
         if (NdotV < 0 || NdotL < 0) return V3{0, 0, 0};
         V3 wh = normalize(r.wi + r.wo);
@@ -342,12 +353,14 @@ ND V3 bsdf_eval(const DevBsdf &b, const BRec &r) {
     }
 }
 
+template <bool FULL = true>
 ND float bsdf_pdf(const DevBsdf &b, const BRec &r) {
     switch (b.type) {
     case NORI_BSDF_DIFFUSE:  // diffuse.cpp:85-98
         if (r.measure != kMeasureSolidAngle || r.wi.z <= 0 || r.wo.z <= 0) return 0.0f;
         return kInvPi * r.wo.z;
     case NORI_BSDF_MICROFACET: {  // microfacet.cpp:93-106
+        if constexpr (!FULL) return 0.0f;
         float c = r.wo.z;
         if (c <= 0.0f) return 0.0f;
         V3 n = normalize(r.wi + r.wo);
@@ -355,6 +368,7 @@ ND float bsdf_pdf(const DevBsdf &b, const BRec &r) {
         return b.ks * mt + (1 - b.ks) * (c * kInvPi);
     }
     case NORI_BSDF_DISNEY: {  // disney.cpp:117-129
+        if constexpr (!FULL) return 0.0f;
         float c = r.wo.z;
         if (c <= 0.0f) return 0.0f;
         V3 n = normalize(r.wi + r.wo);
@@ -367,13 +381,14 @@ ND float bsdf_pdf(const DevBsdf &b, const BRec &r) {
 }
 
 // Returns the sample weight; r.wo / r.measure are set as the reference sets them.
+template <bool FULL = true>
 ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
     switch (b.type) {
     case NORI_BSDF_DIFFUSE:  // diffuse.cpp:101-116
         if (r.wi.z <= 0) return V3{0, 0, 0};
         r.measure = kMeasureSolidAngle;
         r.wo = sq_cosine_hemisphere(s);
-        return albedo_at(b, r.uv);
+        return albedo_at<FULL>(b, r.uv);
     case NORI_BSDF_MIRROR:  // mirror.cpp:39-55
         if (r.wi.z <= 0) return V3{0, 0, 0};
         r.wo = V3{-r.wi.x, -r.wi.y, r.wi.z};
@@ -400,6 +415,7 @@ ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
         return V3{1, 1, 1};
     }
     case NORI_BSDF_MICROFACET: {  // microfacet.cpp:109-131
+        if constexpr (!FULL) return V3{0, 0, 0};
         if (r.wi.z <= 0.0f) return V3{0, 0, 0};
         if (s.x < b.ks) {
             V3 n = sq_beckmann(V2{s.x / b.ks, s.y}, b.alpha);
@@ -409,9 +425,10 @@ ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
         }
         float c = r.wo.z;
         if (c <= 0.f) return V3{0, 0, 0};
-        return (bsdf_eval(b, r) * c) / bsdf_pdf(b, r);
+        return (bsdf_eval<FULL>(b, r) * c) / bsdf_pdf<FULL>(b, r);
     }
     case NORI_BSDF_DISNEY: {  // disney.cpp:132-155
+        if constexpr (!FULL) return V3{0, 0, 0};
         if (r.wi.z <= 0.0f) return V3{0, 0, 0};
         if (s.x <= b.metallic) {
             V3 n = sq_gtr2(V2{s.x / b.metallic, s.y}, b.d_alpha);
@@ -421,7 +438,7 @@ ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
         }
         float c = r.wo.z;
         if (c <= 0.0f) return V3{0, 0, 0};
-        return (bsdf_eval(b, r) * c) / bsdf_pdf(b, r);
+        return (bsdf_eval<FULL>(b, r) * c) / bsdf_pdf<FULL>(b, r);
     }
     }
     return V3{0, 0, 0};

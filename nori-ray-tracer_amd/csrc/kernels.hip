@@ -883,13 +883,14 @@ struct SurfHit {
 
 // setHitInformation: mesh.cpp:122-170, sphere.cpp:78-93 (shading frame and
 // texture coordinates; a mesh without UVs keeps the barycentrics in its.uv).
+template <bool FULL = true>
 ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, V3 o, V3 d) {
     SurfHit h;
     h.shape = (int)S.prim_shape[prim];
     const DevShape &sh = S.shapes[h.shape];
     // only a textured albedo reads the texture coordinates (BRec.uv): the
     // sphere's atan2/acos are skipped for every other BSDF
-    const bool need_uv = S.bsdfs[sh.bsdf].tex != NORI_TEXTURE_CONSTANT || sh.nmap;
+    const bool need_uv = FULL && (S.bsdfs[sh.bsdf].tex != NORI_TEXTURE_CONSTANT || sh.nmap);
     h.uv = V2{u, v};
     if (sh.type == NORI_SHAPE_SPHERE) {
         h.p = o + d * t;
@@ -915,7 +916,7 @@ ND SurfHit surface(const DevScene &S, uint32_t prim, float t, float u, float v, 
         if (sh.has_normals) {
             V3 n = (ld3(S.nrm[i0]) * bx + ld3(S.nrm[i1]) * u) + ld3(S.nrm[i2]) * v;
             h.sh = frame_from(normalize(n));
-            if (sh.nmap) {  // NormalMap::eval (normalmap.cpp:95-134): 2 * byte / 255 - 1, normalized
+            if (FULL && sh.nmap) {  // NormalMap::eval (normalmap.cpp:95-134): 2 * byte / 255 - 1, normalized
                 const V3 t = texel_rgb(texel_at(sh.nmap, sh.nm_w, sh.nm_h, sh.nm_wrap, h.uv));
                 const V3 m = V3{2.0f * t.x - 1.0f, 2.0f * t.y - 1.0f, 2.0f * t.z - 1.0f};
                 h.sh = frame_from(to_world(h.sh, normalize(m)));
@@ -1003,12 +1004,14 @@ ND V3 env_sample(const DevScene &S, const DevEmitter &e, V2 smp, V3 &wi) {
 }
 
 // AreaEmitter (arealight.cpp:39-76) or EnvironmentMap
+template <bool FULL = true>
 ND float emitter_pdf(const DevScene &S, const DevEmitter &e, V3 n, V3 wi) {
-    if (e.type == NORI_EMITTER_ENVMAP) return env_pdf(S, e, wi);
+    if (FULL && e.type == NORI_EMITTER_ENVMAP) return env_pdf(S, e, wi);
     return dot(n, -wi) > 0.0f ? S.shapes[e.shape].area_norm : 0.0f;
 }
+template <bool FULL = true>
 ND V3 emitter_eval(const DevScene &S, const DevEmitter &e, V3 n, V3 wi) {
-    if (e.type == NORI_EMITTER_ENVMAP) return env_eval(S, e, wi);
+    if (FULL && e.type == NORI_EMITTER_ENVMAP) return env_eval(S, e, wi);
     return dot(n, -wi) > 0.0f ? V3{e.radiance[0], e.radiance[1], e.radiance[2]} : V3{0, 0, 0};
 }
 // Shape::sampleSurface: Mesh (mesh.cpp:40-58, DiscretePDF::sampleReuse
@@ -1047,6 +1050,7 @@ ND void sample_surface(const DevScene &S, const DevShape &sh, V2 smp, V3 &p, V3 
 // (thinlens.cpp:120-147) and AdvancedCamera (advancedCamera.cpp:85-157: barrel
 // distortion, uniform-disk lens, per-channel focus shift with chromatic
 // aberration, channel = 0..2 then; -1 otherwise).  Eigen column order.
+template <bool FULL = true>
 ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel, V3 &o, V3 &d, float &mint,
                       float &maxt, float *invz_out = nullptr) {
     const float *m = S.s2c;
@@ -1059,7 +1063,7 @@ ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel,
     V3 dl = normalize(nearP);
     float w = 0.0f;
     bool chroma = false;
-    if (S.cam_type == NORI_CAMERA_ADVANCED) {
+    if (FULL && S.cam_type == NORI_CAMERA_ADVANCED) {
         const float k1 = S.distortion[0], k2 = S.distortion[1];
         if (k1 != 0.0f || k2 != 0.0f) {  // Newton iterations for the undistorted radius
             const float ux = nearP.x / nearP.z, uy = nearP.y / nearP.z;
@@ -1084,7 +1088,7 @@ ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel,
     const float invZ = 1.0f / dl.z;
     const float *c = S.c2w;
     V3 lo = V3{0, 0, 0};
-    if (S.cam_type != NORI_CAMERA_PERSPECTIVE && (S.lens_radius > 0.0f || chroma)) {
+    if (FULL && S.cam_type != NORI_CAMERA_PERSPECTIVE && (S.lens_radius > 0.0f || chroma)) {
         V2 pl = S.cam_type == NORI_CAMERA_THINLENS ? sq_concentric_disk(ap) : sq_uniform_disk(ap);
         pl = V2{S.lens_radius * pl.x, S.lens_radius * pl.y};
         const float ft = S.focal / dl.z;
@@ -1253,15 +1257,16 @@ struct NeeSample {
 // Emitter::sample of one emitter from x with the 2D sample s2: radiance over
 // pdf (not yet scaled by the emitter count), direction, area-measure pdf and
 // the shadow ray's maxt.
+template <bool FULL = true>
 ND NeeSample emitter_sample_one(const DevScene &S, const DevEmitter &E, V3 x, V2 s2) {
     NeeSample r;
-    if (E.type == NORI_EMITTER_POINT || E.type == NORI_EMITTER_SPOT) {
+    if (FULL && (E.type == NORI_EMITTER_POINT || E.type == NORI_EMITTER_SPOT)) {
         r.Li = point_sample(E, x, r.wi, r.maxt);
         r.pdf_em = 1.0f;  // PDF_VALUE (pointlight.cpp:32-35) / lRec.pdf (spotlight.cpp:54-57)
         r.p = V3{E.position[0], E.position[1], E.position[2]};
         return r;
     }
-    if (E.type == NORI_EMITTER_ENVMAP) {
+    if (FULL && E.type == NORI_EMITTER_ENVMAP) {
         r.Li = env_sample(S, E, s2, r.wi);
         r.pdf_em = env_pdf(S, E, r.wi);
         r.maxt = kEnvTFar;               // shadow ray (ref, wi, Epsilon, T_FAR)
@@ -1272,21 +1277,22 @@ ND NeeSample emitter_sample_one(const DevScene &S, const DevEmitter &E, V3 x, V2
     sample_surface(S, S.shapes[E.shape], s2, r.p, ln);
     const V3 dv = r.p - x;
     r.wi = normalize(dv);
-    r.pdf_em = emitter_pdf(S, E, ln, r.wi);
+    r.pdf_em = emitter_pdf<FULL>(S, E, ln, r.wi);
     const float att = dot(ln, -r.wi) / dot(dv, dv);
-    r.Li = r.pdf_em > 0.0f ? (emitter_eval(S, E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
+    r.Li = r.pdf_em > 0.0f ? (emitter_eval<FULL>(S, E, ln, r.wi) * att) / r.pdf_em : V3{0, 0, 0};
     r.maxt = norm(dv) - kEps;
     return r;
 }
 // Next-event estimation of the path integrators: one emitter chosen uniformly
 // (Scene::getRandomEmitter, scene.h:68-74), Li scaled by the emitter count.
+template <bool FULL = true>
 ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
     const float ul = next1D(rng);
     const uint32_t N = S.num_emitters;
     uint32_t li = (uint32_t)floorf((float)N * ul);
     if (li > N - 1) li = N - 1;
     const V2 s2 = next2D(rng);
-    NeeSample r = emitter_sample_one(S, S.emitters[li], x, s2);
+    NeeSample r = emitter_sample_one<FULL>(S, S.emitters[li], x, s2);
     r.Li = r.Li * (float)N;
     return r;
 }
@@ -1352,7 +1358,7 @@ ND bool skip_nee(const DevScene &S, const DevBsdf &B, const V3 &beta) {
 // the surface vertex does path_mis-style emission and NEE, both weighted by
 // transmittance.  ps.prev carries the pdf for w_mats at the next emitter hit
 // (1/4pi after a scattering event, -1 after a discrete lobe).
-template <bool ATOMIC>
+template <bool ATOMIC, bool FULL = true>
 ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
     so.emit = false;
     const uint32_t prim = __float_as_uint(h.y);
@@ -1360,14 +1366,14 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     SurfHit hs;
     float tmax = INF_F;
     if (inter) {
-        hs = surface(S, prim, h.x, h.z, h.w, ps.o, ps.d);
+        hs = surface<FULL>(S, prim, h.x, h.z, h.w, ps.o, ps.d);
         tmax = norm(hs.p - ps.o);
     }
     V3 mp;
     if (medium_sample(S, ps.o, ps.d, ps.rng, tmax, mp)) {
         const V3 wo = sq_uniform_sphere(next2D(ps.rng));
         const float pdf_mat = kInvFourPi;
-        NeeSample ne = nee_sample(S, mp, ps.rng);
+        NeeSample ne = nee_sample<FULL>(S, mp, ps.rng);
         ps.beta = ps.beta * V3{S.albedo[0], S.albedo[1], S.albedo[2]};
         const V3 tr = medium_tr(S, mp, ne.p);
         so.contrib = chan_only(S, ps.chan, ((ps.beta * tr) * ne.Li) * pdf_mat);
@@ -1392,10 +1398,10 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     if (sh.emitter >= 0) {
         const DevEmitter &E = S.emitters[sh.emitter];
         const V3 wi = normalize(hs.p - ps.o);
-        const V3 Le = emitter_eval(S, E, hs.sh.n, wi);
+        const V3 Le = emitter_eval<FULL>(S, E, hs.sh.n, wi);
         float w = 1.0f;
         if (ps.prev >= 0.0f) {
-            const float pe = emitter_pdf(S, E, hs.sh.n, wi);
+            const float pe = emitter_pdf<FULL>(S, E, hs.sh.n, wi);
             w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
         }
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
@@ -1404,15 +1410,15 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     if (skip_nee(S, B, ps.beta)) {
         pcg_skip(ps.rng, 3);
     } else {
-        NeeSample ne = nee_sample(S, hs.p, ps.rng);
+        NeeSample ne = nee_sample<FULL>(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
         br.uv = hs.uv;
         br.wo = to_local(hs.sh, ne.wi);
         br.measure = kMeasureSolidAngle;
         const float theta = smax(0.0f, br.wo.z);
-        const V3 f = bsdf_eval(B, br);
-        const float pdf_mat = bsdf_pdf(B, br);
+        const V3 f = bsdf_eval<FULL>(B, br);
+        const float pdf_mat = bsdf_pdf<FULL>(B, br);
         const float w_ems = (pdf_mat + ne.pdf_em) > 0.0f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
         const V3 tr = medium_tr(S, hs.p, ne.p);
         so.contrib = chan_only(S, ps.chan, ((((ps.beta * w_ems) * f) * theta) * ne.Li) * tr);
@@ -1430,10 +1436,10 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     br.uv = hs.uv;
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
-    const V3 w = bsdf_sample(B, br, next2D(ps.rng));
+    const V3 w = bsdf_sample<FULL>(B, br, next2D(ps.rng));
     if (is_zero(w)) return false;  // deviation D1
     ps.beta = ps.beta * w;
-    const float pm = bsdf_pdf(B, br);
+    const float pm = bsdf_pdf<FULL>(B, br);
     ps.prev = br.measure == kMeasureDiscrete ? -1.0f : pm;
     ps.o = hs.p;
     ps.d = to_world(hs.sh, br.wo);
@@ -1445,24 +1451,24 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
 // One vertex of PathMisIntegrator::Li (path_mis.cpp:32-97) or
 // PathMatsIntegrator::Li (path_mats.cpp:26-57) given the closest hit of the
 // current ray.  Returns true if the path continues (ps holds the new ray).
-template <int INTEG, bool ATOMIC>
+template <int INTEG, bool ATOMIC, bool FULL = true>
 ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
-    if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol<ATOMIC>(S, ps, h, rec, so);
+    if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol<ATOMIC, FULL>(S, ps, h, rec, so);
     so.emit = false;
     uint32_t prim = __float_as_uint(h.y);
     if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
-    SurfHit hs = surface(S, prim, h.x, h.z, h.w, ps.o, ps.d);
+    SurfHit hs = surface<FULL>(S, prim, h.x, h.z, h.w, ps.o, ps.d);
     const DevShape &sh = S.shapes[hs.shape];
     const DevBsdf &B = S.bsdfs[sh.bsdf];
     if (sh.emitter >= 0) {  // emission (path_mis.cpp:35-39, path_mats.cpp:31-35)
         const DevEmitter &E = S.emitters[sh.emitter];
         V3 wi = normalize(hs.p - ps.o);
-        V3 Le = emitter_eval(S, E, hs.sh.n, wi);
+        V3 Le = emitter_eval<FULL>(S, E, hs.sh.n, wi);
         V3 Ladd;
         if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
             float w = 1.0f;  // w_mats (path_mis.cpp:87-97)
             if (ps.prev >= 0.0f) {
-                float pe = emitter_pdf(S, E, hs.sh.n, wi);
+                float pe = emitter_pdf<FULL>(S, E, hs.sh.n, wi);
                 w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
             }
             Ladd = (ps.beta * w) * Le;
@@ -1480,15 +1486,15 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     if (INTEG == NORI_INTEGRATOR_PATH_MIS && skip_nee(S, B, ps.beta)) {
         pcg_skip(ps.rng, 3);
     } else if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
-        const NeeSample ne = nee_sample(S, hs.p, ps.rng);
+        const NeeSample ne = nee_sample<FULL>(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
         br.uv = hs.uv;
         br.wo = to_local(hs.sh, ne.wi);
         br.measure = kMeasureSolidAngle;
         float theta = smax(0.0f, br.wo.z);
-        V3 f = bsdf_eval(B, br);
-        float pdf_mat = bsdf_pdf(B, br);
+        V3 f = bsdf_eval<FULL>(B, br);
+        float pdf_mat = bsdf_pdf<FULL>(B, br);
         float w_ems = (pdf_mat + ne.pdf_em) > 0.0f ? ne.pdf_em / (pdf_mat + ne.pdf_em) : ne.pdf_em;
         so.contrib = chan_only(S, ps.chan, (((ps.beta * w_ems) * f) * theta) * ne.Li);
         so.emit = !is_zero(so.contrib);  // a zero contribution adds nothing (NaN still goes)
@@ -1512,12 +1518,12 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     br.measure = kMeasureSolidAngle;
     V3 w = V3{0.7f, 0.7f, 0.7f};
 #else
-    V3 w = bsdf_sample(B, br, next2D(ps.rng));
+    V3 w = bsdf_sample<FULL>(B, br, next2D(ps.rng));
 #endif
     if (is_zero(w)) return false;  // deviation D1: zero-weight samples end the path
     ps.beta = ps.beta * w;
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
-        float pm = bsdf_pdf(B, br);
+        float pm = bsdf_pdf<FULL>(B, br);
         ps.prev = br.measure == kMeasureDiscrete ? -1.0f : pm;
     }
     ps.o = hs.p;
@@ -1530,6 +1536,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
 // New camera sample for work id w (render.cpp:98-126 + independent.cpp).
 // pix = wd.pixels[w mod M], loaded by the caller (early: a load issued
 // after the path stores would wait for them too -- vmcnt counts in order)
+template <bool FULL = true>
 ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t pix, PathState &ps, float4 *rec) {
     uint32_t pass = w / wd.M;
     uint32_t W = (uint32_t)S.W;
@@ -1538,7 +1545,7 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t p
     wave_seed(ps.rng, wd.seed, sid);
     V2 jit = next2D(ps.rng);
     const V2 ap = next2D(ps.rng);  // apertureSample (render.cpp:99)
-    camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, -1, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
+    camera_sample<FULL>(S, (float)x + jit.x, (float)y + jit.y, ap, -1, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
     ps.cam = true;
     ps.chan = 0;
     ps.beta = V3{1, 1, 1};
@@ -1551,6 +1558,7 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t p
 // with the next channel's camera ray (render.cpp:106-121: the three rays share
 // the pixel and aperture samples, their Li calls consume the sampler in turn,
 // so the pcg32 state simply continues).
+template <bool FULL = true>
 ND void next_channel(const DevScene &S, const WorkDesc &wd, PathState &ps) {
     const uint32_t pass = ps.work / wd.M, pix = wd.pixels[ps.work - pass * wd.M];
     const uint32_t W = (uint32_t)S.W, y = pix / W, x = pix - y * W;
@@ -1559,7 +1567,7 @@ ND void next_channel(const DevScene &S, const WorkDesc &wd, PathState &ps) {
     const V2 jit = next2D(r);
     const V2 ap = next2D(r);
     ps.chan += 1;
-    camera_sample(S, (float)x + jit.x, (float)y + jit.y, ap, (int)ps.chan, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
+    camera_sample<FULL>(S, (float)x + jit.x, (float)y + jit.y, ap, (int)ps.chan, ps.o, ps.d, ps.mint, ps.maxt, &ps.invz);
     ps.cam = true;
     ps.beta = V3{1, 1, 1};
     ps.prev = -1.0f;
@@ -1591,7 +1599,7 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
 // known to point into LDS the compiler emits ds_read for the table reads; a
 // run-time select between the LDS and the global tables leaves generic
 // pointers, i.e. flat loads (vector-memory latency, both wait counters).
-template <int INTEG, bool TRACE, bool LDS>
+template <int INTEG, bool TRACE, bool LDS, bool FULL>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
@@ -1646,10 +1654,10 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     NORI_SPHASE(0)
 #endif
     if (tid < n_in) {
-        alive = shade_vertex<INTEG, true>(S, ps, hit, rec, so);
+        alive = shade_vertex<INTEG, true, FULL>(S, ps, hit, rec, so);
         ps.cam = false;  // a survivor carries its BSDF-sampled ray (Epsilon, inf)
         if (!alive && S.chroma && ps.chan < 2) {  // the sample's next colour channel
-            next_channel(Sg, wd, ps);
+            next_channel<FULL>(Sg, wd, ps);
             alive = true;
         }
     }
@@ -1710,7 +1718,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         const uint32_t wn = s_w[tid - al_tot];
         if (wn != ~0u) {
             PathState np;
-            regen_path(Sg, wd, wn, s_pix[tid - al_tot], np, rec);
+            regen_path<FULL>(Sg, wd, wn, s_pix[tid - al_tot], np, rec);
             if (TRACE) trace_into(Sg, np, out.hit + q);
             store_path(out, q, np);
         }
@@ -1884,6 +1892,24 @@ ND bool coop_scan(const DevScene &S, const CoopPrim &cp, const TRay &mine, bool 
     return res;
 }
 
+// The chord of a solitary sphere (DevShape::solitary): a ray leaving a point
+// of sphere `sh` that hits the sphere again at t hits nothing else before t,
+// and for a ray that starts on the sphere the root box test of the scan
+// passes (the ball lies inside the scene box by a margin).  Same arithmetic
+// as the scan's sphere test (sphere_hit_nb, the adaptive epsilon of
+// bvh.cpp:412-418), so t is the scan's; false: the caller scans as usual.
+ND bool chord_hit(const DevShape &sh, const PathState &ps, float &t) {
+    TRay r;
+    r.o = ps.o;
+    r.d = ps.d;
+    r.mint = ps.mint;
+    r.maxt = ps.maxt;
+    if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
+    if (r.maxt < r.mint) return false;
+    return sphere_hit_nb(make_float4(sh.center[0], sh.center[1], sh.center[2], 0.0f),
+                         make_float4(sh.radius, 0.0f, 0.0f, 0.0f), r, t);
+}
+
 // At most this many tracing lanes use the cooperative scan (each costs one
 // primitive test per lane and a reduction; the per-lane scan costs n tests).
 #ifndef NORI_COOP_MAX
@@ -1924,7 +1950,7 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #define NORI_FINISH_WAVES 8192
 #endif
 constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
-template <int STACK, int INTEG, bool LDS>  // LDS: the scene blob is staged (scan-mode scenes; see k_shade)
+template <int STACK, int INTEG, bool LDS, bool FULL>  // LDS: the scene blob is staged (scan-mode scenes; see k_shade)
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
                                                         const uint32_t *pre, uint32_t G) {
@@ -2007,7 +2033,14 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         ShadowOut so;
         so.emit = false;
         bool alive = false;
-        if (active) alive = shade_vertex<INTEG, false>(S, ps, h, rec, so);
+        // the shape of the vertex being shaded, if it is a solitary sphere (its
+        // table reads issued before the shading, off the dependency chain)
+        int sol = -1;  // (volumetric: a scattering event moves the origin off the surface)
+        if (INTEG != NORI_INTEGRATOR_VOLUMETRIC && active && __float_as_uint(h.y) != 0xFFFFFFFFu) {
+            const int s0 = (int)S.prim_shape[__float_as_uint(h.y)];
+            sol = S.shapes[s0].solitary ? s0 : -1;
+        }
+        if (active) alive = shade_vertex<INTEG, false, FULL>(S, ps, h, rec, so);
         NORI_PHASE(0)
         {
             TRay r{so.o, so.d, V3{0, 0, 0}, kEps, so.maxt};
@@ -2019,8 +2052,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         }
         NORI_PHASE(1)
         if (active && !alive && S.chroma && ps.chan < 2) {  // the sample's next colour channel
-            next_channel(Sg, wd, ps);
+            next_channel<FULL>(Sg, wd, ps);
             alive = true;
+            sol = -1;  // a camera ray
         }
         if (active && !alive) {
             active = false;
@@ -2041,8 +2075,18 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
         uint32_t p;
         rays += active ? 1u : 0u;
         NORI_PHASE(2)
-        trace(r, active, false, t, p, u, v);
-        if (active) h = make_float4(t, __uint_as_float(p), u, v);
+        // a path leaving a solitary sphere: its chord, if it has one, is the
+        // closest hit (the glass-sphere paths of the tail bounce inside)
+        bool want = active;
+        if (active && sol >= 0) {
+            float tc;
+            if (chord_hit(S.shapes[sol], ps, tc)) {
+                h = make_float4(tc, __uint_as_float(S.shapes[sol].prim_offset), 0.0f, 0.0f);
+                want = false;
+            }
+        }
+        trace(r, want, false, t, p, u, v);
+        if (want) h = make_float4(t, __uint_as_float(p), u, v);
         NORI_PHASE(3)
 #ifdef NORI_PROF_FINISH
         if (lane_id() == 0) atomicAdd(&C->prof[4], 1ull);
@@ -2543,19 +2587,26 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
                    : trace_dispatch<false>(S, rays, n, hits, stack, st);
 }
 
-template <int INTEG>
+template <int INTEG, bool FULL>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
     dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
     if (trace && lds)
-        hipLaunchKernelGGL((k_shade<INTEG, true, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+        hipLaunchKernelGGL((k_shade<INTEG, true, true, FULL>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else if (trace)
-        hipLaunchKernelGGL((k_shade<INTEG, true, false>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+        hipLaunchKernelGGL((k_shade<INTEG, true, false, FULL>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
     else if (lds)
-        hipLaunchKernelGGL((k_shade<INTEG, false, true>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+        hipLaunchKernelGGL((k_shade<INTEG, false, true, FULL>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
-        hipLaunchKernelGGL((k_shade<INTEG, false, false>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+        hipLaunchKernelGGL((k_shade<INTEG, false, false, FULL>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+}
+template <int INTEG>
+static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
+                           const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
+                           uint32_t lds, uint32_t nseg, hipStream_t st) {
+    if (S.basic) shade_dispatch<INTEG, false>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    else shade_dispatch<INTEG, true>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
 }
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
@@ -2673,7 +2724,7 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
     return hipGetLastError();
 }
 
-template <int INTEG>
+template <int INTEG, bool FULL>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                             hipStream_t st) {
@@ -2685,15 +2736,22 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
     switch (stack) {
     case 0:  // LDS-staged when the scene has a blob
         if (S.blob_bytes)
-            hipLaunchKernelGGL((k_finish<0, INTEG, true>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+            hipLaunchKernelGGL((k_finish<0, INTEG, true, FULL>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
         else
-            hipLaunchKernelGGL((k_finish<0, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+            hipLaunchKernelGGL((k_finish<0, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
         break;
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG, false>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
+}
+template <int INTEG>
+static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
+                            const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
+                            hipStream_t st) {
+    if (S.basic) finish_dispatch<INTEG, false>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    else finish_dispatch<INTEG, true>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,

@@ -9,6 +9,7 @@
 // record; after the pool drains, k_splat applies ImageBlock::put.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -291,6 +292,106 @@ void scene_root_box(const nori_scene_desc &d, float rmin[3], float rmax[3]) {
     }
 }
 
+// DevShape::solitary for every sphere: no other primitive comes within a
+// margin of its closed ball and the ball lies inside the scene box (rmin,
+// rmax) by that margin.  Closest point of a triangle to the centre: Ericson,
+// Real-Time Collision Detection 5.1.5, in double precision.
+double point_triangle_dist2(const double p[3], const float *a, const float *b, const float *c) {
+    double ab[3], ac[3], ap[3];
+    for (int k = 0; k < 3; ++k) ab[k] = (double)b[k] - a[k], ac[k] = (double)c[k] - a[k], ap[k] = p[k] - a[k];
+    auto dot = [](const double *x, const double *y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+    auto dist2 = [&](const double q[3]) {
+        double s = 0;
+        for (int k = 0; k < 3; ++k) s += (p[k] - q[k]) * (p[k] - q[k]);
+        return s;
+    };
+    double q[3];
+    const double d1 = dot(ab, ap), d2 = dot(ac, ap);
+    if (d1 <= 0 && d2 <= 0) { for (int k = 0; k < 3; ++k) q[k] = a[k]; return dist2(q); }
+    double bp[3];
+    for (int k = 0; k < 3; ++k) bp[k] = p[k] - b[k];
+    const double d3 = dot(ab, bp), d4 = dot(ac, bp);
+    if (d3 >= 0 && d4 <= d3) { for (int k = 0; k < 3; ++k) q[k] = b[k]; return dist2(q); }
+    const double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+        const double v = d1 / (d1 - d3);
+        for (int k = 0; k < 3; ++k) q[k] = a[k] + v * ab[k];
+        return dist2(q);
+    }
+    double cp[3];
+    for (int k = 0; k < 3; ++k) cp[k] = p[k] - c[k];
+    const double d5 = dot(ab, cp), d6 = dot(ac, cp);
+    if (d6 >= 0 && d5 <= d6) { for (int k = 0; k < 3; ++k) q[k] = c[k]; return dist2(q); }
+    const double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+        const double w = d2 / (d2 - d6);
+        for (int k = 0; k < 3; ++k) q[k] = a[k] + w * ac[k];
+        return dist2(q);
+    }
+    const double va = d3 * d6 - d5 * d4;
+    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+        const double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        for (int k = 0; k < 3; ++k) q[k] = b[k] + w * ((double)c[k] - b[k]);
+        return dist2(q);
+    }
+    const double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
+    for (int k = 0; k < 3; ++k) q[k] = a[k] + ab[k] * v + ac[k] * w;
+    return dist2(q);
+}
+
+void mark_solitary_spheres(const nori_scene_desc &d, const float rmin[3], const float rmax[3],
+                           std::vector<DevShape> &shapes) {
+    if (const char *e = std::getenv("NORI_CHORD"); e && e[0] == '0') return;  // A/B: full scans only
+    for (uint32_t s = 0; s < d.num_shapes; ++s) {
+        const nori_shape_desc &sp = d.shapes[s];
+        if (sp.type != NORI_SHAPE_SPHERE || !(sp.radius > 0.0f)) continue;
+        const double r = sp.radius, c[3] = {sp.center[0], sp.center[1], sp.center[2]};
+        const double margin = 1e-4 * (std::max({std::fabs(c[0]), std::fabs(c[1]), std::fabs(c[2])}) + r);
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; ++k) ok = c[k] - r > (double)rmin[k] + margin && c[k] + r < (double)rmax[k] - margin;
+        const double reach = r + margin;
+        for (uint32_t o = 0; o < d.num_shapes && ok; ++o) {
+            if (o == s) continue;
+            const nori_shape_desc &od = d.shapes[o];
+            if (od.type == NORI_SHAPE_SPHERE) {
+                double dd = 0;
+                for (int k = 0; k < 3; ++k) dd += (c[k] - od.center[k]) * (c[k] - od.center[k]);
+                ok = std::sqrt(dd) > reach + od.radius;
+                continue;
+            }
+            for (uint32_t t = 0; t < od.tri_count && ok; ++t) {
+                const uint32_t *f = d.indices + 3 * (size_t)(od.tri_offset + t);
+                const float *p0 = d.positions + 3 * (size_t)f[0], *p1 = d.positions + 3 * (size_t)f[1],
+                            *p2 = d.positions + 3 * (size_t)f[2];
+                bool far = false;  // quick reject: the triangle's box misses the ball's box
+                for (int k = 0; k < 3; ++k)
+                    far = far || std::min({p0[k], p1[k], p2[k]}) > c[k] + reach || std::max({p0[k], p1[k], p2[k]}) < c[k] - reach;
+                if (!far) ok = point_triangle_dist2(c, p0, p1, p2) > reach * reach;
+            }
+        }
+        shapes[s].solitary = ok ? 1 : 0;
+        if (std::getenv("NORI_DEBUG")) std::fprintf(stderr, "[nori] sphere shape %u: solitary %d\n", s, (int)ok);
+    }
+}
+
+// The path kernels' lite variants (FULL = false) serve scenes made of the
+// basic plugins only: constant-albedo diffuse, mirror and dielectric BSDFs,
+// area lights, the perspective camera, no normal maps.  NORI_BASIC=0 forces
+// the full variants (A/B).
+bool basic_scene(const nori_scene_desc &d) {
+    if (const char *e = std::getenv("NORI_BASIC"); e && e[0] == '0') return false;
+    for (uint32_t i = 0; i < d.num_bsdfs; ++i) {
+        const nori_bsdf_desc &b = d.bsdfs[i];
+        if (b.type != NORI_BSDF_DIFFUSE && b.type != NORI_BSDF_MIRROR && b.type != NORI_BSDF_DIELECTRIC) return false;
+        if (b.type == NORI_BSDF_DIFFUSE && b.albedo_texture != NORI_TEXTURE_CONSTANT) return false;
+    }
+    for (uint32_t i = 0; i < d.num_emitters; ++i)
+        if (d.emitters[i].type != NORI_EMITTER_AREA) return false;
+    for (uint32_t i = 0; i < d.num_shapes; ++i)
+        if (d.shapes[i].normal_map >= 0) return false;
+    return d.camera.camera_type == NORI_CAMERA_PERSPECTIVE;
+}
+
 void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     float rmin[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float rmax[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
@@ -394,6 +495,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         off += ds.prim_count;
     }
     c.num_prims = off;
+    mark_solitary_spheres(d, rmin, rmax, shapes);
     std::vector<DevBsdf> bsdfs(d.num_bsdfs);
     for (uint32_t i = 0; i < d.num_bsdfs; ++i) {
         const nori_bsdf_desc &b = d.bsdfs[i];
@@ -625,6 +727,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.distortion[1] = cam.distortion[1];
     for (int k = 0; k < 3; ++k) S.chromatic[k] = cam.camera_type == NORI_CAMERA_ADVANCED ? cam.chromatic[k] : 0.0f;
     S.chroma = S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f;
+    S.basic = basic_scene(d) ? 1 : 0;
     S.W_max = cam.width > cam.height ? cam.width : cam.height;
     S.av_length = d.av_length;
     filter_table(cam, S.filter);
