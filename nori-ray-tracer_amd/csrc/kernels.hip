@@ -20,6 +20,15 @@
 // (bvh.cpp:404-462) and ImageBlock::put (block.cpp:93-133).
 #include "kernels.h"
 
+// The kernels are compiled in three translation units so that hipcc builds
+// them in parallel: NORI_TU 0 (this file) = everything but the two largest
+// groups, 1 (kernels_shade.hip) = k_shade + launch_shade, 2
+// (kernels_finish.hip) = k_finish + launch_finish.  Templates are shared;
+// each non-template kernel and launcher lives in exactly one unit.
+#ifndef NORI_TU
+#define NORI_TU 0
+#endif
+
 namespace nori {
 
 #define INF_F __builtin_inff()
@@ -1800,6 +1809,7 @@ ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, ui
     }
 }
 
+#if NORI_TU == 0
 // Pending marker for the samples the finisher will splat itself.
 __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg, int sel, float4 *rec) {
     const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
@@ -1807,6 +1817,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg,
     rec[__float_as_uint(Q.ray_d[sg * kSeg + idx].w) & kWorkMask].w = 1.0f;
 }
 
+#endif
 // Cooperative scan (scan-mode scenes, n <= 64 primitives): the rays of the
 // lanes in `want` are traced one after another by the whole wave, lane l
 // testing primitive l against the broadcast ray.  The result is exactly that
@@ -1922,6 +1933,7 @@ constexpr int kCoopMax = NORI_COOP_MAX;
 // bounce) would otherwise cost three launches per bounce.  Waves loop while
 // any lane's path is alive so that the lanes can trace cooperatively.
 // Exclusive prefix of the queued-path counts of the G segments (pre[G] = total).
+#if NORI_TU == 2
 __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint32_t G, uint32_t *pre) {
     __shared__ uint32_t part[1024];
     const uint32_t t = threadIdx.x, per = (G + 1023) / 1024, b = t * per, e = min(G, b + per);
@@ -1943,6 +1955,7 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
     if (t == 1023) pre[G] = part[1023];
 }
 
+#endif
 #ifndef NORI_FINISH_PRIO
 #define NORI_FINISH_PRIO 1
 #endif
@@ -2417,6 +2430,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_photons(DevScene S, uint64_t e0
     if (!STORE) count[i] = (uint32_t)(stored < 0xFFFFFFFFull ? stored : 0xFFFFFFFFull);
 }
 
+#if NORI_TU == 0
 template <bool STORE>
 static void photons_dispatch(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *count, const uint64_t *pre,
                              uint64_t total, float4 *out, int stack, hipStream_t st) {
@@ -2436,6 +2450,7 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
     return hipGetLastError();
 }
 
+#endif
 // ------------------------------------------------------------------ film splat
 #ifndef NORI_SPLAT_DEPTH
 #define NORI_SPLAT_DEPTH 1  // sample records in flight per thread (prefetch depth)
@@ -2567,6 +2582,7 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
 }
 
 // ------------------------------------------------------------------ launchers
+#if NORI_TU == 0
 template <bool ANY>
 static hipError_t trace_dispatch(const DevScene &S, const float4 *rays, uint32_t n, float4 *hits, int stack,
                                  hipStream_t st) {
@@ -2587,6 +2603,8 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
                    : trace_dispatch<false>(S, rays, n, hits, stack, st);
 }
 
+#endif
+#if NORI_TU == 1
 template <int INTEG, bool FULL>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
@@ -2625,6 +2643,8 @@ hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue 
     return hipGetLastError();
 }
 
+#endif
+#if NORI_TU == 0
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
@@ -2724,6 +2744,8 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
     return hipGetLastError();
 }
 
+#endif
+#if NORI_TU == 2
 template <int INTEG, bool FULL>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
@@ -2765,6 +2787,8 @@ hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &
     return hipGetLastError();
 }
 
+#endif
+#if NORI_TU == 0
 template <int INTEG>
 static void direct_dispatch(const DevScene &S, const WorkDesc &wd, float4 *rec, Counters *C, int stack,
                             hipStream_t st) {
@@ -2806,4 +2830,5 @@ hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &s
     return hipGetLastError();
 }
 
+#endif
 }  // namespace nori
