@@ -2025,23 +2025,32 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
                        : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
     };
 #ifdef NORI_PROF_FINISH  // profiling build: clocks of the loop's phases, summed over waves
+    // pt: shader clocks (s_memtime) of every iteration; p1: wall time (s_memrealtime,
+    // 100 MHz) of the late iterations (index >= NORI_PROF_LATE) of long-running
+    // waves, when the device runs little else: the lone-lane bounce
+#ifndef NORI_PROF_LATE
+#define NORI_PROF_LATE 200
+#endif
     uint64_t pt[4] = {0, 0, 0, 0}, pc = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime(), wit = 0;
-    uint64_t p1[4] = {0, 0, 0, 0}, n1 = 0;  // iterations with a single active lane
+    uint64_t p1[4] = {0, 0, 0, 0}, n1 = 0, rc = rt0;
     bool solo = false;
 #define NORI_PHASE(i)                                        \
     {                                                        \
         const uint64_t now = __builtin_amdgcn_s_memtime();   \
         pt[i] += now - pc;                                   \
-        if (solo) p1[i] += now - pc;                         \
         pc = now;                                            \
+        const uint64_t rnow = __builtin_amdgcn_s_memrealtime(); \
+        if (solo) p1[i] += rnow - rc;                        \
+        rc = rnow;                                           \
     }
 #else
 #define NORI_PHASE(i)
 #endif
     while (__ballot(active)) {
 #ifdef NORI_PROF_FINISH
-        solo = __popcll(__ballot(active)) == 1;
+        solo = wit >= NORI_PROF_LATE;
         n1 += solo ? 1 : 0;
+        rc = __builtin_amdgcn_s_memrealtime();
 #endif
         ShadowOut so;
         so.emit = false;

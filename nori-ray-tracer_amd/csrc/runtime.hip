@@ -1332,9 +1332,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                              (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4],
                              (double)(hc.prof[5] >> 20) * 1e-5, hc.prof[5] & 0xFFFFFull);
             if (hc.prof[12])
-                std::fprintf(stderr, "[nori] finisher single-lane iterations: shade %.0f shadow %.0f splat %.0f extend %.0f clocks (%llu)\n",
-                             (double)hc.prof[8] / hc.prof[12], (double)hc.prof[9] / hc.prof[12],
-                             (double)hc.prof[10] / hc.prof[12], (double)hc.prof[11] / hc.prof[12], hc.prof[12]);
+                std::fprintf(stderr, "[nori] finisher late iterations (lone lanes): shade %.0f shadow %.0f splat %.0f extend %.0f ns (%llu)\n",
+                             10.0 * hc.prof[8] / hc.prof[12], 10.0 * hc.prof[9] / hc.prof[12],
+                             10.0 * hc.prof[10] / hc.prof[12], 10.0 * hc.prof[11] / hc.prof[12], hc.prof[12]);
         }
         done_before += wd.total;
     }

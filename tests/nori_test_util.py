@@ -142,6 +142,15 @@ REFERENCE_PNG_PAIRS = [
     ("project/disney/cbox_specular_10.xml", "project/disney_cbox_specular_10.png"),  # specularTint 0.2
     ("project/volumetric/volumetric_no_scatter.xml", "project/volumetric_no_scatter.png"),
     ("project/volumetric/volumetric_with_bb.xml", "project/volumetric_with_bb.png"),  # sigma_t 1, box 0.3
+    # scenes/project/euler/file.png: the C2 scene again, rendered on the Euler cluster
+    ("pa4/cbox/cbox_path_mis.xml", "euler_cbox_path_mis.png"),
+    # scenes/project/windowed sync filter/: the C2 scene through the windowed sinc
+    # filter (rfilter.cpp:123-156); its windowed.png / base_filter.png are plots
+    # of the filter shape, not renders
+    ("project/windowed/cbox_path_mis.xml", "project/windowed_cbox_path_mis.png"),
+    # scenes/project/spotlight/: direct integrator, spotlight over a
+    # checkerboard-textured sphere and plane
+    ("project/spotlight/sphere-texture.xml", "project/spotlight_sphere_texture.png"),
 ]
 
 

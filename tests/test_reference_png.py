@@ -1,9 +1,13 @@
 """The oracle against the reference fork's own LDR renders (SURVEY.md 8(c)
 fixture 7): scenes/pa4/cbox/cbox_path_mis.png (the C2 scene, with its mirror
-and dielectric spheres), the Disney parameter sweeps in scenes/project/disney
-(roughness 0 / 0.3 / 0.5 / 0.8, specularTint 0.2) and the two volumetric
-variants in scenes/project/volumetric (no scattering; a sigma_t = 1 medium
-box of half-size 0.3 around the sphere).  PNG files copied into tests/golden/
+and dielectric spheres) and the same scene rendered on Euler
+(scenes/project/euler/file.png), the Disney parameter sweeps in
+scenes/project/disney (roughness 0 / 0.3 / 0.5 / 0.8, specularTint 0.2), the
+two volumetric variants in scenes/project/volumetric (no scattering; a
+sigma_t = 1 medium box of half-size 0.3 around the sphere), the C2 scene
+through the windowed sinc filter (scenes/project/windowed sync filter/) and
+the spotlight scene (scenes/project/spotlight/sphere-texture.png: direct
+integrator, checkerboard albedo).  PNG files copied into tests/golden/
 as data; each is compared with the scene file committed beside it.
 
 The oracle renders in the reference's stream layout (per-block pcg32, BLOCK
@@ -32,9 +36,15 @@ def _oracle(xml, spp):
     return nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="block", threads=0))
 
 
+# the windowed sinc filter's negative lobes make a 16-spp pixel noisy enough
+# that the [0, 1] clamp of saveToLDR biases the channel means by ~0.5-0.9 %;
+# at 64 spp they are within 0.1 %
+ORACLE_SPP = {"project/windowed/cbox_path_mis.xml": 64}
+
+
 @pytest.mark.parametrize("xml,png", REFERENCE_PNG_PAIRS, ids=[p[1] for p in REFERENCE_PNG_PAIRS])
 def test_oracle_matches_reference_png(built, xml, png):
-    st = compare_to_png(_oracle(xml, 16), png_linear(os.path.join(GOLDEN, png)))
+    st = compare_to_png(_oracle(xml, ORACLE_SPP.get(xml, 16)), png_linear(os.path.join(GOLDEN, png)))
     print(xml, st)
     assert np.all(np.abs(st["mean_ratio"] - 1) < 5e-3), st
     assert st["rel_median"] < 0.015 and st["rel_p95"] < 0.06, st
