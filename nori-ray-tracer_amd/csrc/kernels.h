@@ -90,4 +90,5 @@ hipError_t launch_denoise(const float *img, const float *var, int W, int H, int 
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 
+bool trav_stats_take(unsigned long long out[8]);  // NORI_TRAV_STATS builds (diagnostic)
 }  // namespace nori

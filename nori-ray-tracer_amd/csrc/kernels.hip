@@ -144,7 +144,7 @@ ND bool sphere_hit(const float4 &a, const float4 &b, const TRay &r, float &t) {
     float C = dot(oc, oc) - rad * rad;
     float disc = (B * B - 4 * A * C);
     if (!(disc > 0)) return false;
-    float delta = sqrtf(B * B - 4 * A * C);
+    float delta = sqrt_rn(B * B - 4 * A * C);
     float t1 = (-B - delta) / (2 * A), t2 = (-B + delta) / (2 * A);
     if (r.mint <= t1 && t1 <= r.maxt) { t = t1; return true; }
     if (r.mint <= t2 && t2 <= r.maxt) { t = t2; return true; }
@@ -175,7 +175,7 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
     float B = 2.0f * dot(oc, r.d);
     float C = dot(oc, oc) - rad * rad;
     float disc = (B * B - 4 * A * C);
-    float delta = sqrtf(B * B - 4 * A * C);
+    float delta = sqrt_rn(B * B - 4 * A * C);
     float t1 = (-B - delta) / (2 * A), t2 = (-B + delta) / (2 * A);
     bool h1 = r.mint <= t1 && t1 <= r.maxt, h2 = r.mint <= t2 && t2 <= r.maxt;
     t = h1 ? t1 : t2;
@@ -267,6 +267,24 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
     }
 }
 
+// Primitive records fetched per memory round trip in a BVH leaf.
+#ifndef NORI_LEAF_BATCH
+#define NORI_LEAF_BATCH 1
+#endif
+constexpr int kLeafBatch = NORI_LEAF_BATCH;
+
+// NORI_TRAV_STATS builds (diagnostic): per-ray counts of the BVH walks of
+// k_extend / k_shadow -- inner nodes fetched, leaves entered, primitives
+// tested, rays -- summed over the launches (nori_trav_stats).
+#ifdef NORI_TRAV_STATS
+// (one copy per translation unit: the reader sees unit 0's kernels, i.e.
+// k_extend / k_shadow / k_trace, not the tail finisher)
+static __device__ unsigned long long g_trav_stats[8];
+#define NORI_TSTAT(k, n) (tstat[k] += (n))
+#else
+#define NORI_TSTAT(k, n)
+#endif
+
 // LDS words per lane of a traversal stack of depth STACK: child refs and entry distances.
 // (stack_lds_entries(STACK) entries: the LDS budget stays STACK words, so the
 // occupancy does not change; deeper entries spill to private memory)
@@ -318,8 +336,27 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     uint32_t ref = 0;
     int sp = 0;
     bool found = false;
+#ifdef NORI_TRAV_STATS
+    uint32_t tstat[3] = {0, 0, 0};
+    struct Flush {
+        uint32_t *t;
+        ND ~Flush() {  // per lane (lanes leave the walk at different points)
+            atomicAdd(&g_trav_stats[0], (unsigned long long)t[0]);
+            atomicAdd(&g_trav_stats[1], (unsigned long long)t[1]);
+            atomicAdd(&g_trav_stats[2], (unsigned long long)t[2]);
+            atomicAdd(&g_trav_stats[3], 1ull);
+            const uint32_t v = t[0] + t[1];  // node + leaf visits of this ray
+            atomicMax(&g_trav_stats[4], (unsigned long long)v);
+            if (v > 64) {
+                atomicAdd(&g_trav_stats[5], 1ull);
+                atomicAdd(&g_trav_stats[6], (unsigned long long)v);
+            }
+        }
+    } flush{tstat};
+#endif
     for (;;) {
         if (!(ref & 0x80000000u)) {
+            NORI_TSTAT(0, 1);
             float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
             load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
             float k0, k1, k2, k3;
@@ -366,26 +403,42 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
                 continue;
             }
         } else {
-            uint32_t start = ref & 0x1FFFFFFu, end = start + ((ref >> 25) & 63u) + 1u;
-            for (uint32_t i = start; i < end; ++i) {
-                const float4 *p = S.prims + 3 * (size_t)i;
-                float4 p0 = gld(p), p1 = gld(p + 1);
-                float t = 0, u = 0, v = 0;
-                bool h;
-                if (__float_as_uint(p1.w) == 0u) {
-                    float4 p2 = gld(p + 2);
-                    h = tri_hit(p0, p1, p2, r, t, u, v);
-                } else {
-                    h = sphere_hit(p0, p1, r, t);
-                    u = v = 0.0f;
+            // leaf: the records of NORI_LEAF_BATCH primitives are fetched
+            // together (every record is 48 B, so the third vector is loaded
+            // unconditionally; lanes past the leaf end re-read its last
+            // record) -- one memory round trip per batch instead of one or
+            // two per primitive.  Tested in leaf order, as bvh.cpp:440-452.
+            const uint32_t start = ref & 0x1FFFFFFu, end = start + ((ref >> 25) & 63u) + 1u;
+            NORI_TSTAT(1, 1);
+            NORI_TSTAT(2, end - start);
+            for (uint32_t i0 = start; i0 < end; i0 += kLeafBatch) {
+                float4 q[kLeafBatch][3];
+#pragma unroll
+                for (int k = 0; k < kLeafBatch; ++k) {
+                    const float4 *p = S.prims + 3 * (size_t)min(i0 + (uint32_t)k, end - 1u);
+                    q[k][0] = gld(p);
+                    q[k][1] = gld(p + 1);
+                    q[k][2] = gld(p + 2);
                 }
-                if (h) {
-                    if (ANY) return true;
-                    found = true;
-                    r.maxt = tb = t;
-                    ub = u;
-                    vb = v;
-                    pb = __float_as_uint(p0.w);
+#pragma unroll
+                for (int k = 0; k < kLeafBatch; ++k) {
+                    if (i0 + (uint32_t)k >= end) break;
+                    float t = 0, u = 0, v = 0;
+                    bool h;
+                    if (__float_as_uint(q[k][1].w) == 0u) {
+                        h = tri_hit(q[k][0], q[k][1], q[k][2], r, t, u, v);
+                    } else {
+                        h = sphere_hit(q[k][0], q[k][1], r, t);
+                        u = v = 0.0f;
+                    }
+                    if (h) {
+                        if (ANY) return true;
+                        found = true;
+                        r.maxt = tb = t;
+                        ub = u;
+                        vb = v;
+                        pb = __float_as_uint(q[k][0].w);
+                    }
                 }
             }
         }
@@ -1005,7 +1058,7 @@ ND V3 env_sample(const DevScene &S, const DevEmitter &e, V2 smp, V3 &wi) {
     const float theta = (float)((double)u * M_PI / (double)(e.R - 1));  // invMapIntersect
     const float phi = (float)((double)(v * 2.0f) * M_PI / (double)(e.C - 1));
     wi = normalize(V3{sinf(theta) * cosf(phi), sinf(theta) * sinf(phi), cosf(theta)});
-    const float st2 = 1.0f - wi.z * wi.z, st = st2 <= 0.0f ? 0.0f : sqrtf(st2);  // Frame::sinTheta
+    const float st2 = 1.0f - wi.z * wi.z, st = st2 <= 0.0f ? 0.0f : sqrt_rn(st2);  // Frame::sinTheta
     const float jac = (float)((double)((e.C - 1) * (e.R - 1)) / (2 * (M_PI * M_PI) * (double)st));
     v_pdf = env_pdf(S, e, wi) * jac;
     const V3 c = env_eval(S, e, wi);
@@ -1076,7 +1129,7 @@ ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel,
         const float k1 = S.distortion[0], k2 = S.distortion[1];
         if (k1 != 0.0f || k2 != 0.0f) {  // Newton iterations for the undistorted radius
             const float ux = nearP.x / nearP.z, uy = nearP.y / nearP.z;
-            const float y = sqrtf(ux * ux + uy * uy);
+            const float y = sqrt_rn(ux * ux + uy * uy);
             float r = y, rr, f, df;
             int i = 0;
             for (;;) {
@@ -1294,16 +1347,21 @@ ND NeeSample emitter_sample_one(const DevScene &S, const DevEmitter &E, V3 x, V2
 }
 // Next-event estimation of the path integrators: one emitter chosen uniformly
 // (Scene::getRandomEmitter, scene.h:68-74), Li scaled by the emitter count.
+// (ul, s2: the emitter-choice draw and the 2D light sample, in that order)
 template <bool FULL = true>
-ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
-    const float ul = next1D(rng);
+ND NeeSample nee_sample_u(const DevScene &S, V3 x, float ul, V2 s2) {
     const uint32_t N = S.num_emitters;
     uint32_t li = (uint32_t)floorf((float)N * ul);
     if (li > N - 1) li = N - 1;
-    const V2 s2 = next2D(rng);
     NeeSample r = emitter_sample_one<FULL>(S, S.emitters[li], x, s2);
     r.Li = r.Li * (float)N;
     return r;
+}
+template <bool FULL = true>
+ND NeeSample nee_sample(const DevScene &S, V3 x, Pcg &rng) {
+    const float ul = next1D(rng);
+    const V2 s2 = next2D(rng);
+    return nee_sample_u<FULL>(S, x, ul, s2);
 }
 
 // Chromatic aberration (render.cpp:106-121): a sample's value is
@@ -1457,6 +1515,34 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     return true;
 }
 
+// The random numbers of one path_mis / path_mats vertex, drawn up front from
+// a copy of the stream.  They do not depend on the geometry, so their pcg32
+// chain can run beside the surface and BSDF arithmetic instead of after it
+// (a lone tail path's bounce is one long dependency chain).  path_mis: NEE
+// (emitter choice, 2D light sample), Russian roulette, BSDF sample (2D);
+// path_mats: Russian roulette, BSDF sample.  st_rr / st_all: the stream state
+// after the Russian-roulette draw / after every draw, i.e. what the
+// reference's sampler holds when Li returns at that point (a chromatic
+// aberration sample's next channel continues from it).
+template <int N>
+struct VertexDraws {
+    float u[N];
+    uint64_t st_rr, st_all;
+};
+template <int INTEG>
+ND auto vertex_draws(const Pcg &r) {
+    constexpr int N = INTEG == NORI_INTEGRATOR_PATH_MIS ? 6 : 3;
+    VertexDraws<N> d;
+    Pcg c = r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        d.u[i] = pcg_float(c);
+        if (i == N - 3) d.st_rr = c.state;
+    }
+    d.st_all = c.state;
+    return d;
+}
+
 // One vertex of PathMisIntegrator::Li (path_mis.cpp:32-97) or
 // PathMatsIntegrator::Li (path_mats.cpp:26-57) given the closest hit of the
 // current ray.  Returns true if the path continues (ps holds the new ray).
@@ -1465,7 +1551,10 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol<ATOMIC, FULL>(S, ps, h, rec, so);
     so.emit = false;
     uint32_t prim = __float_as_uint(h.y);
-    if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
+    if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85 (nothing drawn)
+    constexpr bool MIS = INTEG == NORI_INTEGRATOR_PATH_MIS;
+    constexpr int RR = MIS ? 3 : 0;  // index of the Russian-roulette draw
+    const auto dr = vertex_draws<INTEG>(ps.rng);
     SurfHit hs = surface<FULL>(S, prim, h.x, h.z, h.w, ps.o, ps.d);
     const DevShape &sh = S.shapes[hs.shape];
     const DevBsdf &B = S.bsdfs[sh.bsdf];
@@ -1474,7 +1563,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         V3 wi = normalize(hs.p - ps.o);
         V3 Le = emitter_eval<FULL>(S, E, hs.sh.n, wi);
         V3 Ladd;
-        if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
+        if (MIS) {
             float w = 1.0f;  // w_mats (path_mis.cpp:87-97)
             if (ps.prev >= 0.0f) {
                 float pe = emitter_pdf<FULL>(S, E, hs.sh.n, wi);
@@ -1487,15 +1576,11 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         rec_add<ATOMIC>(S, rec, ps, Ladd);
     }
 #ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
-    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
-        (void)next1D(ps.rng);
-        (void)next2D(ps.rng);
-    } else
+    if (false) {
+#else
+    if (MIS && !skip_nee(S, B, ps.beta)) {  // next-event estimation (path_mis.cpp:42-61)
 #endif
-    if (INTEG == NORI_INTEGRATOR_PATH_MIS && skip_nee(S, B, ps.beta)) {
-        pcg_skip(ps.rng, 3);
-    } else if (INTEG == NORI_INTEGRATOR_PATH_MIS) {  // next-event estimation (path_mis.cpp:42-61)
-        const NeeSample ne = nee_sample<FULL>(S, hs.p, ps.rng);
+        const NeeSample ne = nee_sample_u<FULL>(S, hs.p, dr.u[0], V2{dr.u[1], dr.u[2]});
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
         br.uv = hs.uv;
@@ -1512,9 +1597,14 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         so.maxt = ne.maxt;
         so.work = ps.work;
     }
+    // (skip_nee, deviation D10: the three NEE draws are consumed unused)
     // Russian roulette on the red channel (path_mis.cpp:64-69)
     float qrr = smin(ps.beta.x, 0.99f);
-    if (next1D(ps.rng) > qrr) return false;
+    if (dr.u[RR] > qrr) {
+        ps.rng.state = dr.st_rr;
+        return false;
+    }
+    ps.rng.state = dr.st_all;
     ps.beta = ps.beta / qrr;
     BRec br;
     br.wi = to_local(hs.sh, -ps.d);
@@ -1522,16 +1612,15 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
 #ifdef NORI_PROF_NO_SAMPLE  // profiling build only: a cheap reflection instead of BSDF sampling
-    V2 su = next2D(ps.rng);
-    br.wo = V3{su.x - 0.5f, su.y - 0.5f, 0.5f};
+    br.wo = V3{dr.u[RR + 1] - 0.5f, dr.u[RR + 2] - 0.5f, 0.5f};
     br.measure = kMeasureSolidAngle;
     V3 w = V3{0.7f, 0.7f, 0.7f};
 #else
-    V3 w = bsdf_sample<FULL>(B, br, next2D(ps.rng));
+    V3 w = bsdf_sample<FULL>(B, br, V2{dr.u[RR + 1], dr.u[RR + 2]});
 #endif
     if (is_zero(w)) return false;  // deviation D1: zero-weight samples end the path
     ps.beta = ps.beta * w;
-    if (INTEG == NORI_INTEGRATOR_PATH_MIS) {
+    if (MIS) {
         float pm = bsdf_pdf<FULL>(B, br);
         ps.prev = br.measure == kMeasureDiscrete ? -1.0f : pm;
     }
@@ -2822,6 +2911,19 @@ hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Cou
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+// NORI_TRAV_STATS builds: read (and reset) the BVH walk counters; false otherwise.
+bool trav_stats_take(unsigned long long out[8]) {
+#ifdef NORI_TRAV_STATS
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trav_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return false;
+    unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trav_stats), z, sizeof(z));
+    return true;
+#else
+    (void)out;
+    return false;
+#endif
 }
 
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,

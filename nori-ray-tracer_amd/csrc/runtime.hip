@@ -505,6 +505,9 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         for (int k = 0; k < 3; ++k) o.albedo[k] = b.albedo[k], o.kd[k] = b.kd[k], o.base[k] = b.base_color[k];
         o.int_ior = b.int_ior;
         o.ext_ior = b.ext_ior;
+        o.eta_ei = b.ext_ior / b.int_ior;  // the divisions of common.cpp:296 / dielectric.cpp:57-60, done once
+        o.eta_ie = b.int_ior / b.ext_ior;
+        o.inv_eta_ei = 1 / o.eta_ei;
         o.alpha = b.alpha;
         float mk = b.kd[0] < b.kd[1] ? b.kd[1] : b.kd[0];
         mk = mk < b.kd[2] ? b.kd[2] : mk;
@@ -804,10 +807,15 @@ bool debug_log() {
     const char *e = std::getenv("NORI_DEBUG");
     return e && e[0] == '1';
 }
-uint32_t pool_parts() {  // NORI_POOL_PARTS: independent pool parts on their own streams (1..kMaxParts)
+// NORI_POOL_PARTS: independent pool parts on their own streams (1..kMaxParts).
+// Default: 2 for scan-mode scenes, 3 for BVH scenes, whose extension and
+// shadow launches each wait for their slowest walks (C3: 2 parts 619, 3
+// parts 651, 4 parts 499 Msamples/s; 4 streams exceed the hardware queues).
+uint32_t pool_parts(bool bvh) {
+    const uint32_t def = bvh ? 3u : 2u;
     const char *e = std::getenv("NORI_POOL_PARTS");
-    const long v = e ? std::atol(e) : 2;
-    return (uint32_t)(v >= 1 && v <= kMaxParts ? v : 2);
+    const long v = e ? std::atol(e) : (long)def;
+    return (uint32_t)(v >= 1 && v <= kMaxParts ? v : def);
 }
 uint64_t event_every() {  // NORI_EVENT_EVERY: iterations per host event (default 1)
     const char *e = std::getenv("NORI_EVENT_EVERY");
@@ -1168,7 +1176,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     const bool fused = c.stack == 0 && fused_extend();
     const uint64_t every = event_every(), ahead = lookahead("NORI_LOOKAHEAD", kLookahead),
                    ahead_end = lookahead("NORI_LOOKAHEAD_END", kLookaheadEnd);
-    const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(), pool / kSeg));
+    const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(c.stack != 0), pool / kSeg));
     const char *stg = std::getenv("NORI_PART_STAGGER");
     const bool stagger = stg && stg[0] == '1';
     const uint32_t G = pool / kSeg;
@@ -1318,6 +1326,12 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         invalid += hc.invalid;
         if (debug_log())
         {
+            unsigned long long ts[8];
+            if (trav_stats_take(ts) && ts[3])
+                std::fprintf(stderr, "[nori] BVH walks: %llu rays, per ray %.2f inner nodes, %.2f leaves, %.2f primitives; "
+                             "longest walk %llu visits, %llu rays over 64 visits (%.1f visits each)\n",
+                             ts[3], (double)ts[0] / ts[3], (double)ts[1] / ts[3], (double)ts[2] / ts[3], ts[4], ts[5],
+                             ts[5] ? (double)ts[6] / ts[5] : 0.0);
             std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays\n", p0,
                          (unsigned long)iters, hc.finish_paths, hc.finish_max_rays);
             if (hc.prof[6])  // NORI_PROF_SHADE builds
