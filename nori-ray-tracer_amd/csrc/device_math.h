@@ -35,25 +35,7 @@ NHD float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 NHD V3 cross(V3 a, V3 b) {
     return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-// sqrtf, correctly rounded: for x in [2^-96, 2^96) the hardware v_sqrt_f32
-// (~1 ulp) plus one Tuckerman test in each direction (two FMA residuals) --
-// verified bit-identical to the IEEE sqrtf sequence for every float in that
-// range by tools/sqrt_check.hip; outside it (and for 0, inf, NaN, negatives)
-// the IEEE sequence, whose denormal scaling this range never needs.  ~30 ns
-// instead of ~52 ns of dependent latency on a lone lane (tools/latency_probe).
-NHD float sqrt_rn(float x) {
-#ifdef __HIP_DEVICE_COMPILE__
-    if (__builtin_expect(!(x >= 0x1p-96f && x < 0x1p96f), 0)) return sqrtf(x);
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
-    const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
-    const float r = rd <= 0.0f ? sd : s;
-    return ru > 0.0f ? su : r;
-#else
-    return sqrtf(x);
-#endif
-}
-NHD float norm(V3 a) { return sqrt_rn(dot(a, a)); }
+NHD float norm(V3 a) { return sqrtf(dot(a, a)); }
 NHD V3 normalize(V3 a) { return a / norm(a); }  // MatrixBase::normalized()
 NHD float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
 NHD float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
@@ -141,10 +123,10 @@ NHD Frame frame_from(V3 a) {  // frame.h:49-51 + coordinateSystem common.cpp:274
     Frame f;
     f.n = a;
     if (fabsf(a.x) > fabsf(a.y)) {
-        float invLen = 1.0f / sqrt_rn(a.x * a.x + a.z * a.z);
+        float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
         f.t = V3{a.z * invLen, 0.0f, -a.x * invLen};
     } else {
-        float invLen = 1.0f / sqrt_rn(a.y * a.y + a.z * a.z);
+        float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
         f.t = V3{0.0f, a.z * invLen, -a.y * invLen};
     }
     f.s = cross(f.t, a);
@@ -155,7 +137,7 @@ NHD V3 to_world(const Frame &f, V3 v) { return (f.s * v.x + f.t * v.y) + f.n * v
 NHD float tan_theta(V3 v) {  // frame.h:77-82
     float temp = 1 - v.z * v.z;
     if (temp <= 0.0f) return 0.0f;
-    return sqrt_rn(temp) / v.z;
+    return sqrtf(temp) / v.z;
 }
 
 // fresnel (common.cpp:285-314) with etaI / etaT taken from the precomputed
@@ -172,7 +154,7 @@ NHD float fresnel(float cosThetaI, float extIOR, float intIOR, float eta_ei, flo
     }
     float sinThetaTSqr = eta * eta * (1 - cosThetaI * cosThetaI);
     if (sinThetaTSqr > 1.0f) return 1.0f;
-    float cosThetaT = sqrt_rn(1.0f - sinThetaTSqr);
+    float cosThetaT = sqrtf(1.0f - sinThetaTSqr);
     float Rs = (etaI * cosThetaI - etaT * cosThetaT) / (etaI * cosThetaI + etaT * cosThetaT);
     float Rp = (etaT * cosThetaI - etaI * cosThetaT) / (etaT * cosThetaI + etaI * cosThetaT);
     return (Rs * Rs + Rp * Rp) / 2.0f;
@@ -180,7 +162,7 @@ NHD float fresnel(float cosThetaI, float extIOR, float intIOR, float eta_ei, flo
 
 // ---------------------------------------------------------------- warps
 NHD V3 sq_cosine_hemisphere(V2 s) {  // warp.cpp:110-115
-    float theta = acosf(sqrt_rn(1 - (1 - s.x)));
+    float theta = acosf(sqrtf(1 - (1 - s.x)));
     float phi = 2.f * kPi * s.y;
     float st = sinf(theta);
     return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
@@ -216,17 +198,17 @@ NHD V2 sq_concentric_disk(V2 s) {
     return V2{r * cosf(theta), r * sinf(theta)};
 }
 NHD V2 sq_uniform_disk(V2 s) {
-    const float angle = 2 * s.x * kPi, size = sqrt_rn(s.y);
+    const float angle = 2 * s.x * kPi, size = sqrtf(s.y);
     return V2{cosf(angle) * size, sinf(angle) * size};
 }
 NHD V3 sq_uniform_triangle(V2 s) {  // warp.cpp:135-140
-    float su1 = sqrt_rn(s.x);
+    float su1 = sqrtf(s.x);
     float u = 1.f - su1, v = s.y * su1;
     return V3{u, v, 1.f - u - v};
 }
 NHD V3 sq_gtr2(V2 s, float alpha) {  // warp.cpp:180-185
     float a2 = alpha * alpha;  // (float)pow(alpha,2): exact product rounded once
-    float theta = acosf(sqrt_rn((1.0f - s.x) / (1.0f + (a2 - 1.0f) * s.x)));
+    float theta = acosf(sqrtf((1.0f - s.x) / (1.0f + (a2 - 1.0f) * s.x)));
     float phi = 2 * kPi * s.y;
     float st = sinf(theta);
     return V3{st * cosf(phi), st * sinf(phi), cosf(theta)};
@@ -328,7 +310,7 @@ ND float schlick(float u) {  // disney.cpp:25-29: pow(m, 5) in double
 }
 ND float ggx(float NdotV, float alphaG) {  // disney.cpp:31-36
     float a = alphaG * alphaG, b = NdotV * NdotV;
-    return 1 / (NdotV + sqrt_rn(a + b - a * b));
+    return 1 / (NdotV + sqrtf(a + b - a * b));
 }
 ND V3 lerp3(float t, V3 a, V3 c) { return a * (1.0f - t) + c * t; }  // disney.cpp:40-42
 

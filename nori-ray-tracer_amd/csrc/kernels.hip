@@ -144,7 +144,7 @@ ND bool sphere_hit(const float4 &a, const float4 &b, const TRay &r, float &t) {
     float C = dot(oc, oc) - rad * rad;
     float disc = (B * B - 4 * A * C);
     if (!(disc > 0)) return false;
-    float delta = sqrt_rn(B * B - 4 * A * C);
+    float delta = sqrtf(B * B - 4 * A * C);
     float t1 = (-B - delta) / (2 * A), t2 = (-B + delta) / (2 * A);
     if (r.mint <= t1 && t1 <= r.maxt) { t = t1; return true; }
     if (r.mint <= t2 && t2 <= r.maxt) { t = t2; return true; }
@@ -175,7 +175,7 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
     float B = 2.0f * dot(oc, r.d);
     float C = dot(oc, oc) - rad * rad;
     float disc = (B * B - 4 * A * C);
-    float delta = sqrt_rn(B * B - 4 * A * C);
+    float delta = sqrtf(B * B - 4 * A * C);
     float t1 = (-B - delta) / (2 * A), t2 = (-B + delta) / (2 * A);
     bool h1 = r.mint <= t1 && t1 <= r.maxt, h2 = r.mint <= t2 && t2 <= r.maxt;
     t = h1 ? t1 : t2;
@@ -1058,7 +1058,7 @@ ND V3 env_sample(const DevScene &S, const DevEmitter &e, V2 smp, V3 &wi) {
     const float theta = (float)((double)u * M_PI / (double)(e.R - 1));  // invMapIntersect
     const float phi = (float)((double)(v * 2.0f) * M_PI / (double)(e.C - 1));
     wi = normalize(V3{sinf(theta) * cosf(phi), sinf(theta) * sinf(phi), cosf(theta)});
-    const float st2 = 1.0f - wi.z * wi.z, st = st2 <= 0.0f ? 0.0f : sqrt_rn(st2);  // Frame::sinTheta
+    const float st2 = 1.0f - wi.z * wi.z, st = st2 <= 0.0f ? 0.0f : sqrtf(st2);  // Frame::sinTheta
     const float jac = (float)((double)((e.C - 1) * (e.R - 1)) / (2 * (M_PI * M_PI) * (double)st));
     v_pdf = env_pdf(S, e, wi) * jac;
     const V3 c = env_eval(S, e, wi);
@@ -1129,7 +1129,7 @@ ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel,
         const float k1 = S.distortion[0], k2 = S.distortion[1];
         if (k1 != 0.0f || k2 != 0.0f) {  // Newton iterations for the undistorted radius
             const float ux = nearP.x / nearP.z, uy = nearP.y / nearP.z;
-            const float y = sqrt_rn(ux * ux + uy * uy);
+            const float y = sqrtf(ux * ux + uy * uy);
             float r = y, rr, f, df;
             int i = 0;
             for (;;) {
@@ -1515,34 +1515,6 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
     return true;
 }
 
-// The random numbers of one path_mis / path_mats vertex, drawn up front from
-// a copy of the stream.  They do not depend on the geometry, so their pcg32
-// chain can run beside the surface and BSDF arithmetic instead of after it
-// (a lone tail path's bounce is one long dependency chain).  path_mis: NEE
-// (emitter choice, 2D light sample), Russian roulette, BSDF sample (2D);
-// path_mats: Russian roulette, BSDF sample.  st_rr / st_all: the stream state
-// after the Russian-roulette draw / after every draw, i.e. what the
-// reference's sampler holds when Li returns at that point (a chromatic
-// aberration sample's next channel continues from it).
-template <int N>
-struct VertexDraws {
-    float u[N];
-    uint64_t st_rr, st_all;
-};
-template <int INTEG>
-ND auto vertex_draws(const Pcg &r) {
-    constexpr int N = INTEG == NORI_INTEGRATOR_PATH_MIS ? 6 : 3;
-    VertexDraws<N> d;
-    Pcg c = r;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        d.u[i] = pcg_float(c);
-        if (i == N - 3) d.st_rr = c.state;
-    }
-    d.st_all = c.state;
-    return d;
-}
-
 // One vertex of PathMisIntegrator::Li (path_mis.cpp:32-97) or
 // PathMatsIntegrator::Li (path_mats.cpp:26-57) given the closest hit of the
 // current ray.  Returns true if the path continues (ps holds the new ray).
@@ -1551,10 +1523,8 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol<ATOMIC, FULL>(S, ps, h, rec, so);
     so.emit = false;
     uint32_t prim = __float_as_uint(h.y);
-    if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85 (nothing drawn)
+    if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
     constexpr bool MIS = INTEG == NORI_INTEGRATOR_PATH_MIS;
-    constexpr int RR = MIS ? 3 : 0;  // index of the Russian-roulette draw
-    const auto dr = vertex_draws<INTEG>(ps.rng);
     SurfHit hs = surface<FULL>(S, prim, h.x, h.z, h.w, ps.o, ps.d);
     const DevShape &sh = S.shapes[hs.shape];
     const DevBsdf &B = S.bsdfs[sh.bsdf];
@@ -1576,11 +1546,14 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         rec_add<ATOMIC>(S, rec, ps, Ladd);
     }
 #ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
-    if (false) {
-#else
-    if (MIS && !skip_nee(S, B, ps.beta)) {  // next-event estimation (path_mis.cpp:42-61)
+    if (MIS) {
+        pcg_skip(ps.rng, 3);
+    } else
 #endif
-        const NeeSample ne = nee_sample_u<FULL>(S, hs.p, dr.u[0], V2{dr.u[1], dr.u[2]});
+    if (MIS && skip_nee(S, B, ps.beta)) {
+        pcg_skip(ps.rng, 3);  // deviation D10: the three NEE draws, unused
+    } else if (MIS) {  // next-event estimation (path_mis.cpp:42-61)
+        const NeeSample ne = nee_sample<FULL>(S, hs.p, ps.rng);
         BRec br;
         br.wi = to_local(hs.sh, -ps.d);
         br.uv = hs.uv;
@@ -1597,14 +1570,9 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         so.maxt = ne.maxt;
         so.work = ps.work;
     }
-    // (skip_nee, deviation D10: the three NEE draws are consumed unused)
     // Russian roulette on the red channel (path_mis.cpp:64-69)
     float qrr = smin(ps.beta.x, 0.99f);
-    if (dr.u[RR] > qrr) {
-        ps.rng.state = dr.st_rr;
-        return false;
-    }
-    ps.rng.state = dr.st_all;
+    if (next1D(ps.rng) > qrr) return false;
     ps.beta = ps.beta / qrr;
     BRec br;
     br.wi = to_local(hs.sh, -ps.d);
@@ -1612,11 +1580,12 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
 #ifdef NORI_PROF_NO_SAMPLE  // profiling build only: a cheap reflection instead of BSDF sampling
-    br.wo = V3{dr.u[RR + 1] - 0.5f, dr.u[RR + 2] - 0.5f, 0.5f};
+    V2 su = next2D(ps.rng);
+    br.wo = V3{su.x - 0.5f, su.y - 0.5f, 0.5f};
     br.measure = kMeasureSolidAngle;
     V3 w = V3{0.7f, 0.7f, 0.7f};
 #else
-    V3 w = bsdf_sample<FULL>(B, br, V2{dr.u[RR + 1], dr.u[RR + 2]});
+    V3 w = bsdf_sample<FULL>(B, br, next2D(ps.rng));
 #endif
     if (is_zero(w)) return false;  // deviation D1: zero-weight samples end the path
     ps.beta = ps.beta * w;
@@ -1697,11 +1666,14 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
 // known to point into LDS the compiler emits ds_read for the table reads; a
 // run-time select between the LDS and the global tables leaves generic
 // pointers, i.e. flat loads (vector-memory latency, both wait counters).
-template <int INTEG, bool TRACE, bool LDS, bool FULL>
+template <int INTEG, bool TRACE, bool LDS, int VAR>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
     static_assert(kShadeBlock == kSeg, "one shade thread per segment slot");
+    // VAR: 0 basic plugins only (FULL = false), 1 full, 2 full + chromatic
+    // aberration (the per-channel continuation is compiled in only then)
+    constexpr bool FULL = VAR != 0, CHROMA = VAR == 2;
     __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64], s_w[kSeg], s_pix[kSeg];
 #if NORI_SORT_OCTANT
     __shared__ uint32_t s_oc[8 * (kShadeBlock / 64)];
@@ -1754,7 +1726,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     if (tid < n_in) {
         alive = shade_vertex<INTEG, true, FULL>(S, ps, hit, rec, so);
         ps.cam = false;  // a survivor carries its BSDF-sampled ray (Epsilon, inf)
-        if (!alive && S.chroma && ps.chan < 2) {  // the sample's next colour channel
+        if (CHROMA && !alive && ps.chan < 2) {  // the sample's next colour channel
             next_channel<FULL>(Sg, wd, ps);
             alive = true;
         }
@@ -2052,7 +2024,7 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #define NORI_FINISH_WAVES 8192
 #endif
 constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
-template <int STACK, int INTEG, bool LDS, bool FULL>  // LDS: the scene blob is staged (scan-mode scenes; see k_shade)
+template <int STACK, int INTEG, bool LDS, int VAR>  // LDS: the scene blob is staged (scan-mode scenes); VAR: see k_shade
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
                                                         const uint32_t *pre, uint32_t G) {
@@ -2064,6 +2036,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
     // render waits for the longest path, and a lane's bounce costs the sum of
     // the branches its wave-mates take: few paths per wave keep that chain
     // close to the lone-lane latency from its first bounce on.
+    constexpr bool FULL = VAR != 0, CHROMA = VAR == 2;
     const uint32_t n = pre[G];
     const uint32_t K = kFinishWaves ? min(64u, max(1u, (n + kFinishWaves - 1) / kFinishWaves)) : 64u;
     if (blockIdx.x * (kTraceBlock / 64) * K >= n) return;  // whole block idle
@@ -2162,7 +2135,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             if (so.emit && !occluded) ps.L = ps.L + so.contrib;  // so.work == ps.work
         }
         NORI_PHASE(1)
-        if (active && !alive && S.chroma && ps.chan < 2) {  // the sample's next colour channel
+        if (CHROMA && active && !alive && ps.chan < 2) {  // the sample's next colour channel
             next_channel<FULL>(Sg, wd, ps);
             alive = true;
             sol = -1;  // a camera ray
@@ -2703,26 +2676,27 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 
 #endif
 #if NORI_TU == 1
-template <int INTEG, bool FULL>
+template <int INTEG, int VAR>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
     dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
     if (trace && lds)
-        hipLaunchKernelGGL((k_shade<INTEG, true, true, FULL>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+        hipLaunchKernelGGL((k_shade<INTEG, true, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else if (trace)
-        hipLaunchKernelGGL((k_shade<INTEG, true, false, FULL>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+        hipLaunchKernelGGL((k_shade<INTEG, true, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
     else if (lds)
-        hipLaunchKernelGGL((k_shade<INTEG, false, true, FULL>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+        hipLaunchKernelGGL((k_shade<INTEG, false, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
-        hipLaunchKernelGGL((k_shade<INTEG, false, false, FULL>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+        hipLaunchKernelGGL((k_shade<INTEG, false, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
 }
 template <int INTEG>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
-    if (S.basic) shade_dispatch<INTEG, false>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
-    else shade_dispatch<INTEG, true>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    if (S.basic) shade_dispatch<INTEG, 0>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    else if (S.chroma) shade_dispatch<INTEG, 2>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    else shade_dispatch<INTEG, 1>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
 }
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
@@ -2844,7 +2818,7 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 
 #endif
 #if NORI_TU == 2
-template <int INTEG, bool FULL>
+template <int INTEG, int VAR>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                             hipStream_t st) {
@@ -2856,22 +2830,23 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
     switch (stack) {
     case 0:  // LDS-staged when the scene has a blob
         if (S.blob_bytes)
-            hipLaunchKernelGGL((k_finish<0, INTEG, true, FULL>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+            hipLaunchKernelGGL((k_finish<0, INTEG, true, VAR>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
         else
-            hipLaunchKernelGGL((k_finish<0, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+            hipLaunchKernelGGL((k_finish<0, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
         break;
-    case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    default: hipLaunchKernelGGL((k_finish<64, INTEG, false, FULL>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
 }
 template <int INTEG>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                             hipStream_t st) {
-    if (S.basic) finish_dispatch<INTEG, false>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
-    else finish_dispatch<INTEG, true>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    if (S.basic) finish_dispatch<INTEG, 0>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    else if (S.chroma) finish_dispatch<INTEG, 2>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    else finish_dispatch<INTEG, 1>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,

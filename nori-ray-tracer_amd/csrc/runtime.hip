@@ -808,11 +808,14 @@ bool debug_log() {
     return e && e[0] == '1';
 }
 // NORI_POOL_PARTS: independent pool parts on their own streams (1..kMaxParts).
-// Default: 2 for scan-mode scenes, 3 for BVH scenes, whose extension and
-// shadow launches each wait for their slowest walks (C3: 2 parts 619, 3
-// parts 651, 4 parts 499 Msamples/s; 4 streams exceed the hardware queues).
+// Default 3: each part's launches wait for their own slowest walks / longest
+// lanes, and three streams keep the chip busy in between (C3: 2 parts 619,
+// 3 parts 651, 4 parts 499 Msamples/s -- 4 streams exceed the hardware
+// queues; table scene 517 -> 555; C2 4563 -> 4658; 64-spp share 3026 ->
+// 3089; C4 and C5 within 1 %).
 uint32_t pool_parts(bool bvh) {
-    const uint32_t def = bvh ? 3u : 2u;
+    (void)bvh;
+    const uint32_t def = 3u;
     const char *e = std::getenv("NORI_POOL_PARTS");
     const long v = e ? std::atol(e) : (long)def;
     return (uint32_t)(v >= 1 && v <= kMaxParts ? v : def);
