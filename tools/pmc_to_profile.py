@@ -58,7 +58,7 @@ def main():
                                  "profiled_ms_per_launch": fk[k][2] / n}
     # SQ instruction counters (tools/gpu_pmc_sq.sh groups), when collected
     import glob
-    for d in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"pmcsq_{tag}_*"))):
+    for d in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"pmcsq_{tag}_[0-9]*"))):
         path = os.path.join(d, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
