@@ -1,14 +1,14 @@
 #!/bin/bash
 # Interleaved A/B benchmark: each configuration (an env assignment, "-" = none)
 # runs once per round for $REPS rounds; prints every value and the median.
-# usage: REPS=3 tools/gpu_ab.sh "- NORI_POOL_PARTS=1 NORI_POOL_PARTS=3" [bench args]
+# usage: REPS=3 tools/gpu_ab.sh "- NORI_POOL_PARTS=1 NORI_POOL_PARTS=3,NORI_X=1" [bench args]
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 cfgs=$1; shift
 reps=${REPS:-3}
 for r in $(seq 1 $reps); do
   for c in $cfgs; do
-    if [ "$c" = "-" ]; then envs=""; else envs="$c"; fi
+    if [ "$c" = "-" ]; then envs=""; else envs="${c//,/ }"; fi  # a,b: two assignments
     env $envs timeout -k 10 300 python bench.py --no-cpu-baseline --no-parity "$@" > gpurun_out/ab.log 2>&1
     rc=$?; if [ $rc -ne 0 ]; then echo "$c rc=$rc"; tail -3 gpurun_out/ab.log; exit $rc; fi
     v=$(grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; print(round(json.loads(sys.stdin.read())['value'],1))")
