@@ -39,11 +39,6 @@ struct DevShape {
     // this sphere that hits it again hits nothing before (the chord is inside
     // the ball), so the tail finisher takes that hit without a scene scan
     int32_t solitary;
-    // solitary dielectric sphere: a path reflected back inside it along a
-    // chord shorter than this (a grazing chord: Fresnel reflectance >= 1/2,
-    // so the path is likely to stay trapped for many bounces) is handed to
-    // the express finisher (kernels.hip k_express); 0: never
-    float express_tc;
     const uint32_t *nmap;         // RGBX8 texels in global memory, or null
 };
 
@@ -160,24 +155,6 @@ constexpr uint32_t kCameraRay = 0x80000000u;  // ray_d.w flag: mint/maxt from th
 constexpr uint32_t kChanShift = 29;            // ray_d.w bits 29-30: colour channel (chromatic aberration)
 constexpr uint32_t kWorkMask = (1u << kChanShift) - 1u;  // record index (work ids < 2^29: runtime chunking)
 
-// Express hand-off of trapped paths (kernels.hip k_express): k_shade appends
-// a path as one entry of kExpressEntry float4 (ray_o, ray_d as in PathQueue;
-// the chord it is about to bounce along as its hit; thr; the sample's record
-// so far with the pcg32 state's high word in .w), stored write-through, and
-// publishes it through ready[]; k_express launches on the side stream claim
-// and finish the published entries.  ctl[kExpressReserved]: entries reserved
-// by k_shade (may exceed cap: those hand-offs were refused),
-// ctl[kExpressClaimed]: entries claimed (each on its own 128-byte line).
-struct ExpressQueue {
-    float4 *entry;
-    uint32_t *ready;
-    uint32_t *ctl;
-    uint32_t cap;    // 0: no express hand-off in this render
-    uint32_t batch;  // entries a wave claims at a time (1..64)
-};
-constexpr uint32_t kExpressEntry = 5;
-constexpr uint32_t kExpressReserved = 0, kExpressClaimed = 32, kExpressCtlWords = 64;
-
 struct ShadowQueue {
     float4 *ray_o;
     float4 *ray_d;
@@ -241,12 +218,7 @@ struct Counters {
     unsigned long long prof[15];   // profiling builds only (NORI_PROF_SHADE / NORI_PROF_FINISH): phase clocks
     uint32_t finish_paths;         // paths completed by the tail finisher
     uint32_t finish_max_rays;      // most rays traced by one finisher path
-    uint32_t express_paths;        // trapped paths completed by the express finisher
-    uint32_t express_rays;         // rays they traced there
-    uint32_t express_dropped;      // hand-offs refused: the express queue was full
-    uint32_t express_max_rays;     // most rays traced by one express path
-    uint32_t express_max_spin;     // longest wait for an entry's publication (polls)
-    uint32_t pad2[25];
+    uint32_t pad2[30];
     unsigned long long direct_rays[2];  // one-bounce integrators: closest-hit, shadow rays
     unsigned long long pad3[14];
 };

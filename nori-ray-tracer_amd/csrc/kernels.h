@@ -50,7 +50,7 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 // launch_extend is then skipped).
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                        uint32_t nseg, const ExpressQueue &xq, hipStream_t st);
+                        uint32_t nseg, hipStream_t st);
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
@@ -63,11 +63,7 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 // (pre: G + 1 words of scratch for the prefix over the segment counts)
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
-                         const ExpressQueue &xq, hipStream_t st);
-// The express finisher of trapped paths (dev_scene.h ExpressQueue): `waves`
-// waves claim the entries published so far, finish and splat them, and exit.
-hipError_t launch_express(const DevScene &S, const ExpressQueue &xq, float4 *rec, const WorkDesc &wd, float *film,
-                          Counters *C, int stack, uint32_t waves, hipStream_t st);
+                         hipStream_t st);
 // Persistent BVH traversal (k_trace_pt): `blocks` resident work-groups pull
 // queue segments through ctr[0..1] (zero before the first launch; each launch
 // leaves them zero).  Stacks 8, 16, 32 only (BVH scenes).

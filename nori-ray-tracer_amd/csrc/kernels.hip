@@ -1204,7 +1204,9 @@ ND uint64_t sample_id(const DevScene &S, const WorkDesc &wd, uint32_t w) {
     const uint32_t pass = w / wd.M;
     return (uint64_t)(wd.pass_begin + pass) * ((uint64_t)S.W * (uint64_t)S.H) + wd.pixels[w - pass * wd.M];
 }
-ND void unpack_path(const DevScene &S, const WorkDesc &wd, float4 ro, float4 rd, float4 th, uint32_t sh, PathState &ps) {
+ND void load_path(const DevScene &S, const WorkDesc &wd, const PathQueue &Q, uint32_t q, PathState &ps) {
+    const float4 ro = Q.ray_o[q], rd = Q.ray_d[q], th = Q.thr[q];
+    const uint32_t sh = Q.rng[q];
     ps.o = ld3(ro);
     ps.d = ld3(rd);
     const uint32_t wf = __float_as_uint(rd.w);
@@ -1218,9 +1220,6 @@ ND void unpack_path(const DevScene &S, const WorkDesc &wd, float4 ro, float4 rd,
     ps.beta = ld3(th);
     ps.rng.state = ((uint64_t)sh << 32) | __float_as_uint(th.w);
     ps.rng.inc = (sample_id(S, wd, ps.work) << 1u) | 1u;  // pcg32 seed(initstate, initseq = sid)
-}
-ND void load_path(const DevScene &S, const WorkDesc &wd, const PathQueue &Q, uint32_t q, PathState &ps) {
-    unpack_path(S, wd, Q.ray_o[q], Q.ray_d[q], Q.thr[q], Q.rng[q], ps);
 }
 ND void store_path(const PathQueue &Q, uint32_t i, const PathState &ps) {
     Q.ray_o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.cam ? ps.invz : ps.prev);
@@ -1651,36 +1650,6 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
     *hit = make_float4(t, __uint_as_float(p), u, v);
 }
 
-// A 16-byte write-through (sc1) store: two 8-byte agent-scope stores, so a
-// consumer on another XCD sees the bytes without a release fence (an L2
-// write-back) on this side.
-ND void store_wt(float4 *p, float4 v) {
-    typedef __attribute__((address_space(1))) unsigned long long gu64;
-    gu64 *g = (gu64 *)p;
-    __hip_atomic_store(g, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The chord of a solitary sphere (DevShape::solitary): a ray leaving a point
-// of sphere `sh` that hits the sphere again at t hits nothing else before t,
-// and for a ray that starts on the sphere the root box test of the scan
-// passes (the ball lies inside the scene box by a margin).  Same arithmetic
-// as the scan's sphere test (sphere_hit_nb, the adaptive epsilon of
-// bvh.cpp:412-418), so t is the scan's; false: the caller scans as usual.
-ND bool chord_hit(const DevShape &sh, const PathState &ps, float &t) {
-    TRay r;
-    r.o = ps.o;
-    r.d = ps.d;
-    r.mint = ps.mint;
-    r.maxt = ps.maxt;
-    if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
-    if (r.maxt < r.mint) return false;
-    return sphere_hit_nb(make_float4(sh.center[0], sh.center[1], sh.center[2], 0.0f),
-                         make_float4(sh.radius, 0.0f, 0.0f, 0.0f), r, t);
-}
-
 #ifndef NORI_SHADE_WAVES
 #define NORI_SHADE_WAVES 5
 #endif
@@ -1700,7 +1669,7 @@ ND bool chord_hit(const DevShape &sh, const PathState &ps, float &t) {
 template <int INTEG, bool TRACE, bool LDS, int VAR>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
-             float4 *rec, Counters *C, uint32_t lds_bytes, ExpressQueue xq) {
+             float4 *rec, Counters *C, uint32_t lds_bytes) {
     static_assert(kShadeBlock == kSeg, "one shade thread per segment slot");
     // VAR: 0 basic plugins only (FULL = false), 1 full, 2 full + chromatic
     // aberration (the per-channel continuation is compiled in only then)
@@ -1755,53 +1724,11 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     NORI_SPHASE(0)
 #endif
     if (tid < n_in) {
-        // express candidate: the vertex lies on an express sphere
-        // (DevShape::express_tc) and the ray arrived from inside it
-        int xs = -1;
-        if (INTEG != NORI_INTEGRATOR_VOLUMETRIC && xq.cap && __float_as_uint(hit.y) != 0xFFFFFFFFu) {
-            const int s0 = (int)S.prim_shape[__float_as_uint(hit.y)];
-            const DevShape &sh0 = S.shapes[s0];
-            if (sh0.express_tc > 0.0f &&
-                dot(ps.d, (ps.o + ps.d * hit.x) - V3{sh0.center[0], sh0.center[1], sh0.center[2]}) > 0.0f)
-                xs = s0;
-        }
         alive = shade_vertex<INTEG, true, FULL>(S, ps, hit, rec, so);
         ps.cam = false;  // a survivor carries its BSDF-sampled ray (Epsilon, inf)
         if (CHROMA && !alive && ps.chan < 2) {  // the sample's next colour channel
             next_channel<FULL>(Sg, wd, ps);
             alive = true;
-        }
-        // ... and was reflected back inside along a grazing chord: a path
-        // likely trapped for many bounces (whispering gallery), handed to the
-        // express finisher, which runs it to its end at lone-lane speed
-        // instead of one bounce per wavefront iteration.  No shadow ray is
-        // pending from a dielectric vertex (deviation D10) and those of the
-        // earlier vertices were traced before this launch, so its record is
-        // complete so far; it is marked pending (k_splat skips it).
-        float tc;
-        if (INTEG != NORI_INTEGRATOR_VOLUMETRIC && xs >= 0 && alive && !ps.cam && !so.emit &&
-            chord_hit(S.shapes[xs], ps, tc) && tc < S.shapes[xs].express_tc) {
-            const uint32_t i = atomicAdd(&xq.ctl[kExpressReserved], 1u);
-            if (i < xq.cap) {
-                // the record so far: written by earlier launches only (an
-                // express sphere emits nothing, so this vertex adds nothing)
-                const float4 r0 = rec[ps.work];
-                // published write-through (sc1) and drained before the flag:
-                // no L2 write-back fence (the consumer may run on another XCD)
-                float4 *e = xq.entry + (size_t)kExpressEntry * i;
-                store_wt(e + 0, make_float4(ps.o.x, ps.o.y, ps.o.z, ps.prev));
-                store_wt(e + 1, make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(ps.work | (ps.chan << kChanShift))));
-                store_wt(e + 2, make_float4(tc, __uint_as_float(S.shapes[xs].prim_offset), 0.0f, 0.0f));
-                store_wt(e + 3, make_float4(ps.beta.x, ps.beta.y, ps.beta.z, __uint_as_float((uint32_t)ps.rng.state)));
-                store_wt(e + 4, make_float4(r0.x, r0.y, r0.z, __uint_as_float((uint32_t)(ps.rng.state >> 32))));
-                rec[ps.work].w = 1.0f;  // pending (k_splat skips it; read by later launches only)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)(xq.ready + i), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                alive = false;
-            } else {
-                atomicAdd(&C->express_dropped, 1u);
-            }
         }
     }
     NORI_SPHASE(1)
@@ -2037,6 +1964,24 @@ ND bool coop_scan(const DevScene &S, const CoopPrim &cp, const TRay &mine, bool 
     return res;
 }
 
+// The chord of a solitary sphere (DevShape::solitary): a ray leaving a point
+// of sphere `sh` that hits the sphere again at t hits nothing else before t,
+// and for a ray that starts on the sphere the root box test of the scan
+// passes (the ball lies inside the scene box by a margin).  Same arithmetic
+// as the scan's sphere test (sphere_hit_nb, the adaptive epsilon of
+// bvh.cpp:412-418), so t is the scan's; false: the caller scans as usual.
+ND bool chord_hit(const DevShape &sh, const PathState &ps, float &t) {
+    TRay r;
+    r.o = ps.o;
+    r.d = ps.d;
+    r.mint = ps.mint;
+    r.maxt = ps.maxt;
+    if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
+    if (r.maxt < r.mint) return false;
+    return sphere_hit_nb(make_float4(sh.center[0], sh.center[1], sh.center[2], 0.0f),
+                         make_float4(sh.radius, 0.0f, 0.0f, 0.0f), r, t);
+}
+
 // At most this many tracing lanes use the cooperative scan (each costs one
 // primitive test per lane and a reduction; the per-lane scan costs n tests).
 #ifndef NORI_COOP_MAX
@@ -2079,16 +2024,68 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #define NORI_FINISH_WAVES 8192
 #endif
 constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
-// The tail loop of k_finish and k_express: every active lane's path runs to
-// completion, the wave looping while any lane's path is alive so that the
-// lanes can trace cooperatively; a finished sample is splatted into the film
-// here (k_splat skipped it as pending).  ray_stat: where a lane adds its
-// traced-ray count when its path ends; express: count it as an express path.
-template <int STACK, int INTEG, int VAR, class Trace>
-ND void tail_loop(const DevScene &S, const DevScene &Sg, const WorkDesc &wd, float4 *rec, float *film, Counters *C,
-                  const Trace &trace, PathState &ps, float4 h, bool active, uint32_t *ray_stat, bool express) {
+template <int STACK, int INTEG, bool LDS, int VAR>  // LDS: the scene blob is staged (scan-mode scenes); VAR: see k_shade
+__global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
+                                                        float4 *rec, WorkDesc wd, float *film, Counters *C,
+                                                        const uint32_t *pre, uint32_t G) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
+    extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
+    // the queued paths of all segments, numbered through the prefix `pre`
+    // (k_tail_prefix), K consecutive ones per wave: K = n / kFinishWaves
+    // rounded up, so the tail spreads over about kFinishWaves waves.  The
+    // render waits for the longest path, and a lane's bounce costs the sum of
+    // the branches its wave-mates take: few paths per wave keep that chain
+    // close to the lone-lane latency from its first bounce on.
     constexpr bool FULL = VAR != 0, CHROMA = VAR == 2;
-    uint32_t rays = express && active ? 1u : 0u;  // an express path's chord was not traced
+    const uint32_t n = pre[G];
+    const uint32_t K = kFinishWaves ? min(64u, max(1u, (n + kFinishWaves - 1) / kFinishWaves)) : 64u;
+    if (blockIdx.x * (kTraceBlock / 64) * K >= n) return;  // whole block idle
+    // Each bounce of a tail path is a chain of dependent reads of small
+    // tables; for small scenes they are staged into LDS first so the chain
+    // runs at LDS latency instead of L2 latency.
+    DevScene S = Sg;
+    if constexpr (LDS) {  // the BVH path reads global memory (gld)
+        for (uint32_t i = threadIdx.x; i < Sg.blob_bytes / 16; i += kTraceBlock) blob_lds[i] = Sg.blob[i];
+        __syncthreads();
+        S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
+    }
+    const uint32_t first = (blockIdx.x * kTraceBlock + threadIdx.x) / 64 * K, gid = first + lane_id();
+    if (first >= n) return;  // whole wave idle
+#if NORI_FINISH_PRIO
+    // the film splat runs beside the finisher: its waves must not take the
+    // issue slots of these few latency-bound ones
+    __builtin_amdgcn_s_setprio(3);
+#endif
+    bool active = lane_id() < K && gid < n;
+    uint32_t sg = 0;
+    if (active) {  // segment of path gid: last s with pre[s] <= gid
+        uint32_t lo = 0, hi = G;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= gid) lo = mid;
+            else hi = mid;
+        }
+        sg = lo;
+    }
+    const uint32_t q = sg * kSeg + (active ? gid - pre[sg] : 0u);
+    PathState ps;
+    float4 h = make_float4(0, 0, 0, 0);
+    if (active) {
+        load_path(Sg, wd, Q, q, ps);
+        h = Q.hit[q];
+        ps.L = ld3(rec[ps.work]);
+    }
+    uint32_t rays = 0;
+    const bool coop = STACK == 0 && S.num_prims <= 64;
+    CoopPrim cp;
+    if (coop) cp = coop_load(S);
+    auto trace = [&](const TRay &r, bool want, bool any_hit, float &t, uint32_t &p, float &u, float &v) -> bool {
+        if (coop && __popcll(__ballot(want)) <= kCoopMax)
+            return any_hit ? coop_scan<true>(S, cp, r, want, t, p, u, v) : coop_scan<false>(S, cp, r, want, t, p, u, v);
+        if (!want) return false;
+        return any_hit ? traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)
+                       : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
+    };
 #ifdef NORI_PROF_FINISH  // profiling build: clocks of the loop's phases, summed over waves
     // pt: shader clocks (s_memtime) of every iteration; p1: wall time (s_memrealtime,
     // 100 MHz) of the late iterations (index >= NORI_PROF_LATE) of long-running
@@ -2153,14 +2150,9 @@ ND void tail_loop(const DevScene &S, const DevScene &Sg, const WorkDesc &wd, flo
             V2 jit = next2D(rg);
             // Sg: kernarg filter table (no local copy)
             splat_sample(Sg, film, C, x, y, jit, make_float4(ps.L.x, ps.L.y, ps.L.z, 0.0f), wd.var);
-            atomicAdd(ray_stat, rays);
-            if (express) {
-                atomicAdd(&C->express_paths, 1u);
-                atomicMax(&C->express_max_rays, rays);
-            } else {
-                atomicAdd(&C->finish_paths, 1u);
-                atomicMax(&C->finish_max_rays, rays);
-            }
+            atomicAdd(&seg.stats[sg].w, rays);
+            atomicAdd(&C->finish_paths, 1u);
+            atomicMax(&C->finish_max_rays, rays);
         }
         TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
         float t, u, v;
@@ -2196,173 +2188,6 @@ ND void tail_loop(const DevScene &S, const DevScene &Sg, const WorkDesc &wd, flo
     }
 #endif
 #undef NORI_PHASE
-}
-
-// Claims up to xq.batch of the reserved, unclaimed express entries
-// for this wave: (first index, count); count 0: none left now.
-ND uint2 express_claim(const ExpressQueue &xq) {
-    uint32_t base = 0, n = 0;
-    if (lane_id() == 0) {
-        const uint32_t res =
-            min(__hip_atomic_load(&xq.ctl[kExpressReserved], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), xq.cap);
-        uint32_t head = __hip_atomic_load(&xq.ctl[kExpressClaimed], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (head < res) {  // a failed exchange reloads head: bounded by res - head successes of others
-            const uint32_t want = min(xq.batch, res - head);
-            if (__hip_atomic_compare_exchange_strong(&xq.ctl[kExpressClaimed], &head, head + want, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                base = head;
-                n = want;
-                break;
-            }
-        }
-    }
-    return make_uint2(__builtin_amdgcn_readfirstlane(base), __builtin_amdgcn_readfirstlane(n));
-}
-// Lane l < count: the path of express entry first + l, its record so far in
-// ps.L.  The entry was reserved before this claim; its producer publishes it
-// right after (ready[]), so the wait is short; bounded all the same.
-ND bool express_load(const DevScene &Sg, const WorkDesc &wd, const ExpressQueue &xq, Counters *C, uint2 cl,
-                     PathState &ps, float4 &h) {
-    const bool mine = lane_id() < cl.y;
-    const uint32_t i = cl.x + (mine ? lane_id() : 0u);
-    bool ok = mine;
-    uint32_t spin = 0;
-    // relaxed polls of the flag, then ONE agent-scope acquire (this CU's L1
-    // dropped) before the plain loads of the entry
-    while (ok && !__hip_atomic_load((__attribute__((address_space(1))) uint32_t *)(xq.ready + i), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT)) {
-        if (++spin > (1u << 20)) ok = false;  // never published: cannot happen (bounded rather than hung)
-        else __builtin_amdgcn_s_sleep(2);
-    }
-    if (spin) atomicMax(&C->express_max_spin, spin);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (!ok) return false;
-    const float4 *e = xq.entry + (size_t)kExpressEntry * i;
-    const float4 ro = e[0], rd = e[1], th = e[3], rl = e[4];
-    h = e[2];
-    unpack_path(Sg, wd, ro, rd, th, __float_as_uint(rl.w), ps);
-    ps.L = ld3(rl);
-    return true;
-}
-
-constexpr uint32_t kExpressDrainBlocks = 16;
-
-template <int STACK, int INTEG, bool LDS, int VAR>  // LDS: the scene blob is staged (scan-mode scenes); VAR: see k_shade
-__global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
-                                                        float4 *rec, WorkDesc wd, float *film, Counters *C,
-                                                        const uint32_t *pre, uint32_t G, ExpressQueue xq) {
-    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
-    // the queued paths of all segments, numbered through the prefix `pre`
-    // (k_tail_prefix), K consecutive ones per wave: K = n / kFinishWaves
-    // rounded up, so the tail spreads over about kFinishWaves waves.  The
-    // render waits for the longest path, and a lane's bounce costs the sum of
-    // the branches its wave-mates take: few paths per wave keep that chain
-    // close to the lone-lane latency from its first bounce on.
-    const uint32_t n = pre[G];
-    const uint32_t K = kFinishWaves ? min(64u, max(1u, (n + kFinishWaves - 1) / kFinishWaves)) : 64u;
-    // the first kExpressDrainBlocks work-groups also drain the express
-    // entries nobody has claimed, so they stay even without tail paths
-    const bool drain = xq.cap && blockIdx.x < kExpressDrainBlocks;
-    if (blockIdx.x * (kTraceBlock / 64) * K >= n && !drain) return;  // whole block idle
-    // Each bounce of a tail path is a chain of dependent reads of small
-    // tables; for small scenes they are staged into LDS first so the chain
-    // runs at LDS latency instead of L2 latency.
-    DevScene S = Sg;
-    if constexpr (LDS) {  // the BVH path reads global memory (gld)
-        for (uint32_t i = threadIdx.x; i < Sg.blob_bytes / 16; i += kTraceBlock) blob_lds[i] = Sg.blob[i];
-        __syncthreads();
-        S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
-    }
-    const uint32_t first = (blockIdx.x * kTraceBlock + threadIdx.x) / 64 * K, gid = first + lane_id();
-    if (first >= n && !drain) return;  // whole wave idle
-#if NORI_FINISH_PRIO
-    // the film splat runs beside the finisher: its waves must not take the
-    // issue slots of these few latency-bound ones
-    __builtin_amdgcn_s_setprio(3);
-#endif
-    bool active = lane_id() < K && gid < n;
-    uint32_t sg = 0;
-    if (active) {  // segment of path gid: last s with pre[s] <= gid
-        uint32_t lo = 0, hi = G;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pre[mid] <= gid) lo = mid;
-            else hi = mid;
-        }
-        sg = lo;
-    }
-    const uint32_t q = sg * kSeg + (active ? gid - pre[sg] : 0u);
-    PathState ps;
-    float4 h = make_float4(0, 0, 0, 0);
-    if (active) {
-        load_path(Sg, wd, Q, q, ps);
-        h = Q.hit[q];
-        ps.L = ld3(rec[ps.work]);
-    }
-    const bool coop = STACK == 0 && S.num_prims <= 64;
-    CoopPrim cp;
-    if (coop) cp = coop_load(S);
-    auto trace = [&](const TRay &r, bool want, bool any_hit, float &t, uint32_t &p, float &u, float &v) -> bool {
-        if (coop && __popcll(__ballot(want)) <= kCoopMax)
-            return any_hit ? coop_scan<true>(S, cp, r, want, t, p, u, v) : coop_scan<false>(S, cp, r, want, t, p, u, v);
-        if (!want) return false;
-        return any_hit ? traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)
-                       : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
-    };
-    if (__ballot(active)) tail_loop<STACK, INTEG, VAR>(S, Sg, wd, rec, film, C, trace, ps, h, active, &seg.stats[sg].w, false);
-    // then the express entries not claimed yet (every hand-off of the chunk
-    // was made before this launch)
-    while (drain) {
-        const uint2 cl = express_claim(xq);
-        if (cl.y == 0) break;
-        const bool a = express_load(Sg, wd, xq, C, cl, ps, h);
-        tail_loop<STACK, INTEG, VAR>(S, Sg, wd, rec, film, C, trace, ps, h, a, &C->express_rays, true);
-    }
-}
-
-// The express finisher: launched on the side stream once per wavefront
-// iteration (and once more at the drain, beside k_finish), it claims the
-// express entries published so far and runs each path to its end, then
-// exits -- no wave waits for entries that are not there yet.
-template <int STACK, int INTEG, bool LDS, int VAR>
-__global__ __launch_bounds__(kTraceBlock) void k_express(DevScene Sg, ExpressQueue xq, float4 *rec, WorkDesc wd,
-                                                         float *film, Counters *C) {
-    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    __shared__ uint32_t s_any;
-    extern __shared__ __attribute__((aligned(16))) float4 blob_lds[];
-    if (threadIdx.x == 0) {
-        const uint32_t res =
-            min(__hip_atomic_load(&xq.ctl[kExpressReserved], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), xq.cap);
-        s_any = __hip_atomic_load(&xq.ctl[kExpressClaimed], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < res;
-    }
-    __syncthreads();
-    if (!s_any) return;  // nothing to claim: the whole block exits
-    DevScene S = Sg;
-    if constexpr (LDS) {
-        for (uint32_t i = threadIdx.x; i < Sg.blob_bytes / 16; i += kTraceBlock) blob_lds[i] = Sg.blob[i];
-        __syncthreads();
-        S = scene_in_lds(Sg, reinterpret_cast<const char *>(blob_lds));
-    }
-    __builtin_amdgcn_s_setprio(3);  // few latency-bound waves beside the wavefront's many
-    const bool coop = STACK == 0 && S.num_prims <= 64;
-    CoopPrim cp;
-    if (coop) cp = coop_load(S);
-    auto trace = [&](const TRay &r, bool want, bool any_hit, float &t, uint32_t &p, float &u, float &v) -> bool {
-        if (coop && __popcll(__ballot(want)) <= kCoopMax)
-            return any_hit ? coop_scan<true>(S, cp, r, want, t, p, u, v) : coop_scan<false>(S, cp, r, want, t, p, u, v);
-        if (!want) return false;
-        return any_hit ? traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)
-                       : traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
-    };
-    for (;;) {
-        const uint2 cl = express_claim(xq);
-        if (cl.y == 0) break;
-        PathState ps;
-        float4 h = make_float4(0, 0, 0, 0);
-        const bool a = express_load(Sg, wd, xq, C, cl, ps, h);
-        tail_loop<STACK, INTEG, VAR>(S, Sg, wd, rec, film, C, trace, ps, h, a, &C->express_rays, true);
-    }
 }
 
 // ------------------------------------------------------------------ one-bounce integrators
@@ -2854,40 +2679,38 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 template <int INTEG, int VAR>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                           uint32_t lds, uint32_t nseg, const ExpressQueue &xq, hipStream_t st) {
+                           uint32_t lds, uint32_t nseg, hipStream_t st) {
     dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
     if (trace && lds)
-        hipLaunchKernelGGL((k_shade<INTEG, true, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds, xq);
+        hipLaunchKernelGGL((k_shade<INTEG, true, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else if (trace)
-        hipLaunchKernelGGL((k_shade<INTEG, true, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u, xq);
+        hipLaunchKernelGGL((k_shade<INTEG, true, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
     else if (lds)
-        hipLaunchKernelGGL((k_shade<INTEG, false, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds, xq);
+        hipLaunchKernelGGL((k_shade<INTEG, false, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
-        hipLaunchKernelGGL((k_shade<INTEG, false, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u, xq);
+        hipLaunchKernelGGL((k_shade<INTEG, false, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
 }
 template <int INTEG>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                           uint32_t lds, uint32_t nseg, const ExpressQueue &xq, hipStream_t st) {
-    if (S.basic) shade_dispatch<INTEG, 0>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, xq, st);
-    else if (S.chroma) shade_dispatch<INTEG, 2>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, xq, st);
-    else shade_dispatch<INTEG, 1>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, xq, st);
+                           uint32_t lds, uint32_t nseg, hipStream_t st) {
+    if (S.basic) shade_dispatch<INTEG, 0>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    else if (S.chroma) shade_dispatch<INTEG, 2>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    else shade_dispatch<INTEG, 1>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
 }
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
-                        uint32_t nseg, const ExpressQueue &xq, hipStream_t st) {
+                        uint32_t nseg, hipStream_t st) {
     if (nseg == 0 || wd.b0 + nseg > wd.G) return hipErrorInvalidValue;
     const uint32_t lds = S.blob_bytes <= kShadeLdsMax ? S.blob_bytes : 0u;
     switch (S.integrator) {
     case NORI_INTEGRATOR_PATH_MATS:
-        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, xq, st);
+        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
         break;
     case NORI_INTEGRATOR_VOLUMETRIC:
-        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, xq, st);
+        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
         break;
-    default:
-        shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, xq, st);
-        break;
+    default: shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st); break;
     }
     return hipGetLastError();
 }
@@ -2998,80 +2821,42 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 template <int INTEG, int VAR>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
-                            const ExpressQueue &xq, hipStream_t st) {
+                            hipStream_t st) {
     hipLaunchKernelGGL(k_tail_prefix, dim3(1), dim3(1024), 0, st, seg.cnt[sel], G, pre);
     // enough waves for any path count n <= 256 G (kFinishWaves, or n / 64 <= 4 G when
     // K = 64); the idle blocks exit at once
     constexpr uint32_t wpb = kTraceBlock / 64;  // waves per block
     dim3 g(std::max<uint32_t>(2 * G, (kFinishWaves + wpb - 1) / wpb)), b(kTraceBlock);
-#define NORI_FIN(STK, L, LB) \
-    hipLaunchKernelGGL((k_finish<STK, INTEG, L, VAR>), g, b, LB, st, S, Q, seg, sel, rec, wd, film, C, pre, G, xq)
     switch (stack) {
     case 0:  // LDS-staged when the scene has a blob
-        if (S.blob_bytes) NORI_FIN(0, true, S.blob_bytes);
-        else NORI_FIN(0, false, 0);
+        if (S.blob_bytes)
+            hipLaunchKernelGGL((k_finish<0, INTEG, true, VAR>), g, b, S.blob_bytes, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
+        else
+            hipLaunchKernelGGL((k_finish<0, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G);
         break;
-    case 8: NORI_FIN(8, false, 0); break;
-    case 16: NORI_FIN(16, false, 0); break;
-    case 32: NORI_FIN(32, false, 0); break;
-    default: NORI_FIN(64, false, 0); break;
+    case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    default: hipLaunchKernelGGL((k_finish<64, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
-#undef NORI_FIN
 }
 template <int INTEG>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
-                            const ExpressQueue &xq, hipStream_t st) {
-    if (S.basic) finish_dispatch<INTEG, 0>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, xq, st);
-    else if (S.chroma) finish_dispatch<INTEG, 2>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, xq, st);
-    else finish_dispatch<INTEG, 1>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, xq, st);
+                            hipStream_t st) {
+    if (S.basic) finish_dispatch<INTEG, 0>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    else if (S.chroma) finish_dispatch<INTEG, 2>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+    else finish_dispatch<INTEG, 1>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
-                         const ExpressQueue &xq, hipStream_t st) {
+                         hipStream_t st) {
     if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, xq, st);
+        finish_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else if (S.integrator == NORI_INTEGRATOR_VOLUMETRIC)
-        finish_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, xq, st);
+        finish_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else
-        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, xq, st);
-    return hipGetLastError();
-}
-
-// The express finisher runs the path integrators' surface bounces only (the
-// volumetric integrator makes no hand-off).
-template <int INTEG, int VAR>
-static void express_dispatch(const DevScene &S, const ExpressQueue &xq, float4 *rec, const WorkDesc &wd, float *film,
-                             Counters *C, int stack, uint32_t waves, hipStream_t st) {
-    constexpr uint32_t wpb = kTraceBlock / 64;
-    dim3 g((waves + wpb - 1) / wpb), b(kTraceBlock);
-#define NORI_EXP(STK, L, LB) hipLaunchKernelGGL((k_express<STK, INTEG, L, VAR>), g, b, LB, st, S, xq, rec, wd, film, C)
-    switch (stack) {
-    case 0:
-        if (S.blob_bytes) NORI_EXP(0, true, S.blob_bytes);
-        else NORI_EXP(0, false, 0);
-        break;
-    case 8: NORI_EXP(8, false, 0); break;
-    case 16: NORI_EXP(16, false, 0); break;
-    case 32: NORI_EXP(32, false, 0); break;
-    default: NORI_EXP(64, false, 0); break;
-    }
-#undef NORI_EXP
-}
-template <int INTEG>
-static void express_dispatch(const DevScene &S, const ExpressQueue &xq, float4 *rec, const WorkDesc &wd, float *film,
-                             Counters *C, int stack, uint32_t waves, hipStream_t st) {
-    if (S.basic) express_dispatch<INTEG, 0>(S, xq, rec, wd, film, C, stack, waves, st);
-    else if (S.chroma) express_dispatch<INTEG, 2>(S, xq, rec, wd, film, C, stack, waves, st);
-    else express_dispatch<INTEG, 1>(S, xq, rec, wd, film, C, stack, waves, st);
-}
-hipError_t launch_express(const DevScene &S, const ExpressQueue &xq, float4 *rec, const WorkDesc &wd, float *film,
-                          Counters *C, int stack, uint32_t waves, hipStream_t st) {
-    if (!xq.cap || !waves || S.integrator == NORI_INTEGRATOR_VOLUMETRIC) return hipErrorInvalidValue;
-    if (S.integrator == NORI_INTEGRATOR_PATH_MATS)
-        express_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, xq, rec, wd, film, C, stack, waves, st);
-    else
-        express_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, xq, rec, wd, film, C, stack, waves, st);
+        finish_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     return hipGetLastError();
 }
 

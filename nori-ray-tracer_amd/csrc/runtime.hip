@@ -188,7 +188,7 @@ struct nori_gpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;       // film splat, overlapped with the tail finisher
-    hipEvent_t fork = nullptr, join = nullptr, xjoin = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     hipStream_t parts[kMaxParts] = {};  // parts[0] unused (part 0 runs on `stream`)
     hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
@@ -206,8 +206,6 @@ struct nori_gpu_ctx {
     DevBuf ptctr;                    // persistent traversal work counters, 4 per part
     DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
     DevBuf ph, ph_rgbe, ph_tab, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
-    DevBuf xq[3];                    // express queue (dev_scene.h ExpressQueue): entries, ready flags, counters
-    bool express_scene = false;      // a shape has DevShape::express_tc > 0
     uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
@@ -233,7 +231,6 @@ struct nori_gpu_ctx {
         if (readback) (void)hipHostFree(readback);
         if (fork) (void)hipEventDestroy(fork);
         if (join) (void)hipEventDestroy(join);
-        if (xjoin) (void)hipEventDestroy(xjoin);
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -340,47 +337,6 @@ double point_triangle_dist2(const double p[3], const float *a, const float *b, c
     const double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
     for (int k = 0; k < 3; ++k) q[k] = a[k] + ab[k] * v + ac[k] * w;
     return dist2(q);
-}
-
-// Express spheres (DevShape::express_tc): solitary dielectric spheres.  A
-// path reflected back inside along a chord of length 2 r cos(theta) keeps
-// that angle at every later bounce (a chord of a sphere meets it at equal
-// angles), so its chance of staying inside per bounce is the Fresnel
-// reflectance there; hand-offs are made for reflectance >= NORI_EXPRESS_F
-// (default 1/2), i.e. chords shorter than 2 r cos(theta*), found here with
-// the unpolarised formula of common.cpp:fresnel for the inside (eta = int /
-// ext).  A performance heuristic only: every path's result is the same
-// either way.  Off unless NORI_EXPRESS=1.
-void mark_express_spheres(const nori_scene_desc &d, std::vector<DevShape> &shapes) {
-    const char *e = std::getenv("NORI_EXPRESS");
-    if (!(e && e[0] == '1')) return;  // opt-in (unstable run-to-run)
-    const char *fe = std::getenv("NORI_EXPRESS_F");
-    const double fmin = fe ? std::atof(fe) : 0.5;
-    if (!(fmin > 0.0 && fmin < 1.0)) return;
-    for (uint32_t s = 0; s < d.num_shapes; ++s) {
-        DevShape &sh = shapes[s];
-        if (!sh.solitary || sh.emitter >= 0 || sh.bsdf < 0 || (uint32_t)sh.bsdf >= d.num_bsdfs) continue;
-        const nori_bsdf_desc &b = d.bsdfs[sh.bsdf];
-        if (b.type != NORI_BSDF_DIELECTRIC || !(b.int_ior > 0.0f) || !(b.ext_ior > 0.0f)) continue;
-        const double eta_i = b.int_ior, eta_t = b.ext_ior;  // leaving the sphere
-        auto refl = [&](double ci) {
-            const double st2 = (eta_i / eta_t) * (eta_i / eta_t) * (1.0 - ci * ci);
-            if (st2 >= 1.0) return 1.0;
-            const double ct = std::sqrt(1.0 - st2);
-            const double rs = (eta_i * ci - eta_t * ct) / (eta_i * ci + eta_t * ct);
-            const double rp = (eta_t * ci - eta_i * ct) / (eta_t * ci + eta_i * ct);
-            return 0.5 * (rs * rs + rp * rp);
-        };
-        if (refl(0.0) < fmin) continue;
-        double lo = 0.0, hi = 1.0;  // refl(lo) >= fmin > refl(hi) (reflectance falls with cos)
-        if (refl(hi) >= fmin) continue;
-        for (int it = 0; it < 60; ++it) {
-            const double mid = 0.5 * (lo + hi);
-            (refl(mid) >= fmin ? lo : hi) = mid;
-        }
-        sh.express_tc = (float)(2.0 * sh.radius * lo);
-        if (std::getenv("NORI_DEBUG")) std::fprintf(stderr, "[nori] shape %u: express sphere, chords < %g (cos %.4f)\n", s, sh.express_tc, lo);
-    }
 }
 
 void mark_solitary_spheres(const nori_scene_desc &d, const float rmin[3], const float rmax[3],
@@ -690,9 +646,6 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     c.pos.upload(pos);
     c.nrm.upload(nrm);
     c.prim_shape.upload(prim_shape);
-    mark_express_spheres(d, shapes);
-    c.express_scene = false;
-    for (const DevShape &sh : shapes) c.express_scene |= sh.express_tc > 0.0f;
     c.shapes.upload(shapes);
     c.bsdfs.upload(bsdfs);
     c.emitters.upload(emitters);
@@ -896,21 +849,6 @@ uint32_t splat_passes(uint32_t np, size_t nblocks, uint32_t target_wgs = 256) {
     if (v < 1) v = 1;
     return (uint32_t)std::min<long>(v, np);
 }
-// Express finisher launches (k_express): waves per launch.
-uint32_t express_waves() {
-    const char *w = std::getenv("NORI_EXPRESS_WAVES");
-    const long v = w ? std::atol(w) : 64L;
-    return (uint32_t)std::max<long>(4, std::min<long>(v, 4096));
-}
-// NORI_EXPRESS_BATCH: express entries a wave claims at a time (a wave's
-// bounce costs about the lone-lane latency whatever its lane count, but it
-// runs until its longest path ends)
-uint32_t express_batch() {
-    const char *e = std::getenv("NORI_EXPRESS_BATCH");
-    const long v = e ? std::atol(e) : 1L;
-    return (uint32_t)std::max<long>(1, std::min<long>(v, 64));
-}
-constexpr uint32_t kExpressCap = 1u << 20;  // express entries per chunk of passes (further hand-offs are refused)
 bool overlap_splat() {
     const char *e = std::getenv("NORI_SPLAT_OVERLAP");
     return !(e && e[0] == '0');
@@ -1254,15 +1192,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     std::vector<uint4> hstats(G);
     uint64_t finish_rays = 0, samples_started = 0;
     float *var = var_begin(c, rd);
-    ExpressQueue xq{};
-    const uint32_t xwaves = express_waves();
-    if (c.express_scene && S.integrator != NORI_INTEGRATOR_VOLUMETRIC) {
-        c.xq[0].ensure(16 * (size_t)kExpressEntry * kExpressCap);
-        c.xq[1].ensure(4 * (size_t)kExpressCap);
-        c.xq[2].ensure(4 * (size_t)kExpressCtlWords);
-        xq = ExpressQueue{c.xq[0].as<float4>(), c.xq[1].as<uint32_t>(), c.xq[2].as<uint32_t>(), kExpressCap,
-                          express_batch()};
-    }
     for (uint32_t p0 = 0; p0 < passes && !cancelled; p0 += chunk) {
         uint32_t np = std::min(chunk, passes - p0);
         WorkDesc wd{(uint64_t)np * M, M, rd.pass_begin + p0, c.pixels.as<uint32_t>(), rd.seed, G, c.pinned_dev, 1, 0,
@@ -1274,10 +1203,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         uint32_t empty = 0;
         for (uint32_t b = 0; b < G; ++b) empty += stream_work(wd, b, 0) >= wd.total;
         HIP_TRY(launch_reset(C, empty, seg, G, c.stream));
-        if (xq.cap) {
-            HIP_TRY(hipMemsetAsync(xq.ready, 0, 4 * (size_t)kExpressCap, c.stream));
-            HIP_TRY(hipMemsetAsync(xq.ctl, 0, 4 * (size_t)kExpressCtlWords, c.stream));
-        }
         int last_out = 0;
         // The pool is split into `parts` independent parts (segments never
         // interact), each driven on its own stream: the memory-bound shade
@@ -1307,8 +1232,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         HIP_TRY(hipEventRecord(c.fork, c.stream));  // the part streams start after the resets above
         for (uint32_t h = 1; h < parts; ++h) HIP_TRY(hipStreamWaitEvent(c.parts[h], c.fork, 0));
-        if (xq.cap) HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));  // the express launches, likewise
-        bool xlaunched = false;
         uint64_t lag = (ahead + every - 1) / every;
         const uint64_t lag_end = (ahead_end + every - 1) / every;
         for (uint64_t it = 0;; ++it) {
@@ -1319,7 +1242,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                 const SegState &sg = segh[h];
                 timed_on(st, 2, [&] {
                     return launch_shade(S, Qh[h][in], Qh[h][out], sqh[h], sg, in, wdh[h], c.rec.as<float4>(), C,
-                                        fused, Gp[h], xq, st);
+                                        fused, Gp[h], st);
                 });
                 if (it == 0 && h == 0 && parts > 1 && stagger) {
                     // NORI_PART_STAGGER=1: the other parts start after part 0's first shade
@@ -1337,16 +1260,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                                                   c.pt_grid[1], st)
                                : launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st);
                 });
-            }
-            // the express finisher takes the paths handed off so far (side
-            // stream): a new launch only once the previous one has ended (it
-            // keeps claiming while entries arrive; a launch queued behind a
-            // running one stalled the other queues' dispatch: the parts then
-            // ran one after another)
-            if (xq.cap && (!xlaunched || hipEventQuery(c.xjoin) == hipSuccess)) {
-                HIP_TRY(launch_express(S, xq, c.rec.as<float4>(), wd, film, C, c.stack, xwaves, c.side));
-                HIP_TRY(hipEventRecord(c.xjoin, c.side));
-                xlaunched = true;
             }
             ++iters;
             // an event every `every` iterations (each record adds a gap
@@ -1382,27 +1295,19 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         // the others runs on the side stream while the finisher completes the
         // pending ones and splats each itself.
         // (NORI_SPLAT_OVERLAP=0: splat after the finisher on the same stream.)
-        // (an express launch may still run on the side stream: the splat then
-        // runs on the part-1 stream, idle since the join, and k_finish also
-        // drains the express entries nobody has claimed)
         const bool overlap = overlap_splat();
-        hipStream_t splat_st = overlap ? (xq.cap ? c.parts[1] : c.side) : c.stream;
+        hipStream_t splat_st = overlap ? c.side : c.stream;
         HIP_TRY(launch_mark(Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stream));
         HIP_TRY(hipEventRecord(c.fork, c.stream));
-        HIP_TRY(hipStreamWaitEvent(splat_st, c.fork, 0));
+        HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, splat_passes(np, blocks.size())),
                      c.blocks.as<int4>(), rd.seed, var};
         timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
         timed(4, [&] {
-            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack,
-                                 c.tailpre.as<uint32_t>(), xq, c.stream);
+            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack, c.tailpre.as<uint32_t>(), c.stream);
         });
-        HIP_TRY(hipEventRecord(c.join, splat_st));
+        HIP_TRY(hipEventRecord(c.join, c.side));
         HIP_TRY(hipStreamWaitEvent(c.stream, c.join, 0));
-        if (xlaunched) {  // the last express launch has ended too
-            HIP_TRY(hipEventRecord(c.xjoin, c.side));
-            HIP_TRY(hipStreamWaitEvent(c.stream, c.xjoin, 0));
-        }
         // read-back through pinned staging: both copies queue behind the
         // finisher without a host round trip each (pageable copies stage twice)
         const size_t rb = sizeof(Counters) + 16 * (size_t)G;
@@ -1426,7 +1331,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             finish_rays += st.w;
         }
         invalid += hc.invalid;
-        finish_rays += hc.express_rays;
         if (debug_log())
         {
             unsigned long long ts[8];
@@ -1435,10 +1339,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                              "longest walk %llu visits, %llu rays over 64 visits (%.1f visits each)\n",
                              ts[3], (double)ts[0] / ts[3], (double)ts[1] / ts[3], (double)ts[2] / ts[3], ts[4], ts[5],
                              ts[5] ? (double)ts[6] / ts[5] : 0.0);
-            std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays; "
-                         "express %u paths, %u rays, %u refused, longest %u rays, longest wait %u polls\n", p0,
-                         (unsigned long)iters, hc.finish_paths, hc.finish_max_rays, hc.express_paths, hc.express_rays,
-                         hc.express_dropped, hc.express_max_rays, hc.express_max_spin);
+            std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays\n", p0,
+                         (unsigned long)iters, hc.finish_paths, hc.finish_max_rays);
             if (hc.prof[6])  // NORI_PROF_SHADE builds
                 std::fprintf(stderr, "[nori] shade clocks per wave: loads %.0f shade %.0f compact %.0f store %.0f regen %.0f drain %.0f (%llu waves)\n",
                              (double)hc.prof[0] / hc.prof[6], (double)hc.prof[1] / hc.prof[6],
@@ -1691,7 +1593,6 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
             HIP_TRY(hipEventCreateWithFlags(&c->joins[h], hipEventDisableTiming));
         }
         HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&c->xjoin, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         upload_scene(*c, *d);
         setup_persistent(*c);
