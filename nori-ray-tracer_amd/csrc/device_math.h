@@ -87,6 +87,12 @@ NHD void pcg_seed(Pcg &r, uint64_t initstate, uint64_t initseq) {
 NHD void pcg_skip(Pcg &r, int n) {  // n draws whose values are not needed
     for (int i = 0; i < n; ++i) r.state = r.state * kPcgMult + r.inc;
 }
+// Three draws skipped in one step: s3 = A^3 s + (A^2 + A + 1) inc (mod 2^64),
+// the same state as pcg_skip(r, 3); the increment term does not depend on
+// the state, so the dependent chain is one 64-bit multiply-add instead of three.
+constexpr uint64_t kPcgMult3 = kPcgMult * kPcgMult * kPcgMult;
+constexpr uint64_t kPcgInc3 = kPcgMult * kPcgMult + kPcgMult + 1u;
+NHD void pcg_skip3(Pcg &r) { r.state = r.state * kPcgMult3 + r.inc * kPcgInc3; }
 NHD float pcg_float(Pcg &r) {
     uint32_t u = (pcg_next(r) >> 9) | 0x3f800000u;
     float f;
@@ -387,6 +393,23 @@ ND float bsdf_pdf(const DevBsdf &b, const BRec &r) {
     }
 }
 
+// Dielectric::sample's direction (dielectric.cpp:45-73; weight 1, discrete)
+ND V3 dielectric_wo(const DevBsdf &b, V3 wi, V2 s) {
+    float theta = wi.z;
+    V3 nv = V3{0, 0, 1.0f};
+    if (fresnel(theta, b.ext_ior, b.int_ior, b.eta_ei, b.eta_ie) > s.x) return V3{-wi.x, -wi.y, wi.z};
+    float factor = b.eta_ei;  // ext / int
+    if (theta < 0.0f) {
+        factor = b.inv_eta_ei;  // 1 / factor
+        nv.z *= -1;
+    }
+    V3 part1 = (wi - nv * dot(wi, nv)) * (-factor);
+    double wn = (double)dot(wi, nv);
+    double rad = 1.0 - (double)factor * (double)factor * (1.0 - wn * wn);
+    V3 part2 = (-nv) * (float)sqrt(rad);
+    return normalize(part1 + part2);
+}
+
 // Returns the sample weight; r.wo / r.measure are set as the reference sets them.
 template <bool FULL = true>
 ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
@@ -401,26 +424,10 @@ ND V3 bsdf_sample(const DevBsdf &b, BRec &r, V2 s) {
         r.wo = V3{-r.wi.x, -r.wi.y, r.wi.z};
         r.measure = kMeasureDiscrete;
         return V3{1, 1, 1};
-    case NORI_BSDF_DIELECTRIC: {  // dielectric.cpp:45-73
-        float theta = r.wi.z;
-        V3 nv = V3{0, 0, 1.0f};
-        if (fresnel(theta, b.ext_ior, b.int_ior, b.eta_ei, b.eta_ie) > s.x) {
-            r.wo = V3{-r.wi.x, -r.wi.y, r.wi.z};
-        } else {
-            float factor = b.eta_ei;  // ext / int
-            if (theta < 0.0f) {
-                factor = b.inv_eta_ei;  // 1 / factor
-                nv.z *= -1;
-            }
-            V3 part1 = (r.wi - nv * dot(r.wi, nv)) * (-factor);
-            double wn = (double)dot(r.wi, nv);
-            double rad = 1.0 - (double)factor * (double)factor * (1.0 - wn * wn);
-            V3 part2 = (-nv) * (float)sqrt(rad);
-            r.wo = normalize(part1 + part2);
-        }
+    case NORI_BSDF_DIELECTRIC:  // dielectric.cpp:45-73
+        r.wo = dielectric_wo(b, r.wi, s);
         r.measure = kMeasureDiscrete;
         return V3{1, 1, 1};
-    }
     case NORI_BSDF_MICROFACET: {  // microfacet.cpp:109-131
         if constexpr (!FULL) return V3{0, 0, 0};
         if (r.wi.z <= 0.0f) return V3{0, 0, 0};

@@ -1551,7 +1551,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     } else
 #endif
     if (MIS && skip_nee(S, B, ps.beta)) {
-        pcg_skip(ps.rng, 3);  // deviation D10: the three NEE draws, unused
+        pcg_skip3(ps.rng);  // deviation D10: the three NEE draws, unused
     } else if (MIS) {  // next-event estimation (path_mis.cpp:42-61)
         const NeeSample ne = nee_sample<FULL>(S, hs.p, ps.rng);
         BRec br;
@@ -1595,6 +1595,30 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     }
     ps.o = hs.p;
     ps.d = to_world(hs.sh, br.wo);
+    ps.mint = kEps;
+    ps.maxt = INF_F;
+    return true;
+}
+
+// shade_vertex at a vertex of a solitary, non-emitting dielectric sphere
+// whose next-event estimation is skipped (skip_nee: deviation D10), reduced
+// to the operations that run there -- the same arithmetic in the same order
+// (surface(): hit point, normal, frame; the three skipped NEE draws; Russian
+// roulette; Dielectric::sample; the discrete pdf) without the plugin
+// dispatch: the tail finisher's trapped glass-sphere paths run a chain of
+// these.  t: the chord's closest hit.  Returns false if the path ends.
+template <int INTEG>
+ND bool glass_bounce(const DevShape &sh, const DevBsdf &B, PathState &ps, float t) {
+    const V3 p = ps.o + ps.d * t;
+    const Frame f = frame_from(normalize(p - V3{sh.center[0], sh.center[1], sh.center[2]}));
+    if (INTEG == NORI_INTEGRATOR_PATH_MIS) pcg_skip3(ps.rng);
+    const float qrr = smin(ps.beta.x, 0.99f);
+    if (next1D(ps.rng) > qrr) return false;
+    ps.beta = ps.beta / qrr;  // (times the sample weight 1, exactly)
+    const V3 wo = dielectric_wo(B, to_local(f, -ps.d), next2D(ps.rng));
+    if (INTEG == NORI_INTEGRATOR_PATH_MIS) ps.prev = -1.0f;  // discrete measure
+    ps.o = p;
+    ps.d = to_world(f, wo);
     ps.mint = kEps;
     ps.maxt = INF_F;
     return true;
@@ -2024,6 +2048,10 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #define NORI_FINISH_WAVES 8192
 #endif
 constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
+#ifndef NORI_FINISH_GLASS  // 0: the tail finisher shades glass-sphere vertices generically
+#define NORI_FINISH_GLASS 1
+#endif
+constexpr bool kFinishGlass = NORI_FINISH_GLASS;
 template <int STACK, int INTEG, bool LDS, int VAR>  // LDS: the scene blob is staged (scan-mode scenes); VAR: see k_shade
 __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q, SegState seg, int sel,
                                                         float4 *rec, WorkDesc wd, float *film, Counters *C,
@@ -2124,7 +2152,30 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             const int s0 = (int)S.prim_shape[__float_as_uint(h.y)];
             sol = S.shapes[s0].solitary ? s0 : -1;
         }
-        if (active) alive = shade_vertex<INTEG, false, FULL>(S, ps, h, rec, so);
+        // a vertex on a solitary glass sphere: the chain of its chord bounces
+        // runs here (glass_bounce, chord_hit) until the path leaves the
+        // sphere or ends, or its NEE could no longer be skipped
+        bool shaded = false;  // this iteration's vertex is shaded, ps holds the next ray
+        if (INTEG != NORI_INTEGRATOR_VOLUMETRIC && kFinishGlass && active && sol >= 0) {
+            const DevShape &gs = S.shapes[sol];
+            const DevBsdf &gb = S.bsdfs[gs.bsdf];
+            if (gb.type == NORI_BSDF_DIELECTRIC && gs.emitter < 0) {
+                while (INTEG != NORI_INTEGRATOR_PATH_MIS || skip_nee(S, gb, ps.beta)) {
+                    alive = glass_bounce<INTEG>(gs, gb, ps, h.x);
+                    shaded = true;
+                    if (!alive) break;
+                    float tc;
+                    if (!chord_hit(gs, ps, tc)) {
+                        sol = -1;  // it leaves the sphere: traced below
+                        break;
+                    }
+                    h = make_float4(tc, __uint_as_float(gs.prim_offset), 0.0f, 0.0f);
+                    ++rays;
+                    shaded = false;
+                }
+            }
+        }
+        if (active && !shaded) alive = shade_vertex<INTEG, false, FULL>(S, ps, h, rec, so);
         NORI_PHASE(0)
         {
             TRay r{so.o, so.d, V3{0, 0, 0}, kEps, so.maxt};
