@@ -35,8 +35,32 @@ NHD float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 NHD V3 cross(V3 a, V3 b) {
     return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
+// sqrtf, correctly rounded, in a shorter dependent chain: v_sqrt_f32 (about
+// 1 ulp) then one Tuckerman test each way (29 instead of 52 ns of lone-lane
+// latency, tools/latency_probe.hip).  Bit-identical to the IEEE sqrtf for
+// every float in [2^-96, 2^96) (tools/sqrt_check.hip, exhaustive); the IEEE
+// sequence runs outside that range.  FAST = true selects it in the templates
+// below (the tail finisher's glass-sphere chain, kernels.hip glass_bounce).
+NHD float sqrt_rn(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    if (__builtin_expect(!(x >= 0x1p-96f && x < 0x1p96f), 0)) return sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    const float r = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : r;
+#else
+    return sqrtf(x);
+#endif
+}
+template <bool FAST = false>
+NHD float fsqrt(float x) {
+    if constexpr (FAST) return sqrt_rn(x);
+    else return sqrtf(x);
+}
 NHD float norm(V3 a) { return sqrtf(dot(a, a)); }
-NHD V3 normalize(V3 a) { return a / norm(a); }  // MatrixBase::normalized()
+template <bool FAST = false>
+NHD V3 normalize(V3 a) { return a / fsqrt<FAST>(dot(a, a)); }  // MatrixBase::normalized()
 NHD float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
 NHD float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
 NHD float maxc(V3 a) { return smax(smax(a.x, a.y), a.z); }
@@ -125,14 +149,15 @@ NHD V2 next2D(Pcg &r) {
 struct Frame {
     V3 s, t, n;
 };
+template <bool FAST = false>
 NHD Frame frame_from(V3 a) {  // frame.h:49-51 + coordinateSystem common.cpp:274-283
     Frame f;
     f.n = a;
     if (fabsf(a.x) > fabsf(a.y)) {
-        float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
+        float invLen = 1.0f / fsqrt<FAST>(a.x * a.x + a.z * a.z);
         f.t = V3{a.z * invLen, 0.0f, -a.x * invLen};
     } else {
-        float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
+        float invLen = 1.0f / fsqrt<FAST>(a.y * a.y + a.z * a.z);
         f.t = V3{0.0f, a.z * invLen, -a.y * invLen};
     }
     f.s = cross(f.t, a);
@@ -148,6 +173,7 @@ NHD float tan_theta(V3 v) {  // frame.h:77-82
 
 // fresnel (common.cpp:285-314) with etaI / etaT taken from the precomputed
 // quotients (eta_ei = extIOR / intIOR, eta_ie = intIOR / extIOR)
+template <bool FAST = false>
 NHD float fresnel(float cosThetaI, float extIOR, float intIOR, float eta_ei, float eta_ie) {
     float etaI = extIOR, etaT = intIOR, eta = eta_ei;
     if (extIOR == intIOR) return 0.0f;
@@ -160,7 +186,7 @@ NHD float fresnel(float cosThetaI, float extIOR, float intIOR, float eta_ei, flo
     }
     float sinThetaTSqr = eta * eta * (1 - cosThetaI * cosThetaI);
     if (sinThetaTSqr > 1.0f) return 1.0f;
-    float cosThetaT = sqrtf(1.0f - sinThetaTSqr);
+    float cosThetaT = fsqrt<FAST>(1.0f - sinThetaTSqr);
     float Rs = (etaI * cosThetaI - etaT * cosThetaT) / (etaI * cosThetaI + etaT * cosThetaT);
     float Rp = (etaT * cosThetaI - etaI * cosThetaT) / (etaT * cosThetaI + etaI * cosThetaT);
     return (Rs * Rs + Rp * Rp) / 2.0f;
@@ -394,10 +420,11 @@ ND float bsdf_pdf(const DevBsdf &b, const BRec &r) {
 }
 
 // Dielectric::sample's direction (dielectric.cpp:45-73; weight 1, discrete)
+template <bool FAST = false>
 ND V3 dielectric_wo(const DevBsdf &b, V3 wi, V2 s) {
     float theta = wi.z;
     V3 nv = V3{0, 0, 1.0f};
-    if (fresnel(theta, b.ext_ior, b.int_ior, b.eta_ei, b.eta_ie) > s.x) return V3{-wi.x, -wi.y, wi.z};
+    if (fresnel<FAST>(theta, b.ext_ior, b.int_ior, b.eta_ei, b.eta_ie) > s.x) return V3{-wi.x, -wi.y, wi.z};
     float factor = b.eta_ei;  // ext / int
     if (theta < 0.0f) {
         factor = b.inv_eta_ei;  // 1 / factor
@@ -407,7 +434,7 @@ ND V3 dielectric_wo(const DevBsdf &b, V3 wi, V2 s) {
     double wn = (double)dot(wi, nv);
     double rad = 1.0 - (double)factor * (double)factor * (1.0 - wn * wn);
     V3 part2 = (-nv) * (float)sqrt(rad);
-    return normalize(part1 + part2);
+    return normalize<FAST>(part1 + part2);
 }
 
 // Returns the sample weight; r.wo / r.measure are set as the reference sets them.

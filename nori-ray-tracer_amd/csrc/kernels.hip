@@ -168,6 +168,7 @@ ND bool tri_hit_nb(const float4 &a, const float4 &b, const float4 &c, const TRay
     return !(det > -1e-8f && det < 1e-8f) && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) &&
            t >= r.mint && t <= r.maxt;
 }
+template <bool FAST = false>
 ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t) {
     V3 oc = r.o - ld3(a);
     float rad = b.x;
@@ -175,7 +176,7 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
     float B = 2.0f * dot(oc, r.d);
     float C = dot(oc, oc) - rad * rad;
     float disc = (B * B - 4 * A * C);
-    float delta = sqrtf(B * B - 4 * A * C);
+    float delta = fsqrt<FAST>(B * B - 4 * A * C);
     float t1 = (-B - delta) / (2 * A), t2 = (-B + delta) / (2 * A);
     bool h1 = r.mint <= t1 && t1 <= r.maxt, h2 = r.mint <= t2 && t2 <= r.maxt;
     t = h1 ? t1 : t2;
@@ -1607,15 +1608,19 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
 // roulette; Dielectric::sample; the discrete pdf) without the plugin
 // dispatch: the tail finisher's trapped glass-sphere paths run a chain of
 // these.  t: the chord's closest hit.  Returns false if the path ends.
+#ifndef NORI_GLASS_FAST_SQRT  // 0: IEEE sqrtf sequence in the glass chain too
+#define NORI_GLASS_FAST_SQRT 1
+#endif
+constexpr bool kGlassFast = NORI_GLASS_FAST_SQRT;
 template <int INTEG>
 ND bool glass_bounce(const DevShape &sh, const DevBsdf &B, PathState &ps, float t) {
     const V3 p = ps.o + ps.d * t;
-    const Frame f = frame_from(normalize(p - V3{sh.center[0], sh.center[1], sh.center[2]}));
+    const Frame f = frame_from<kGlassFast>(normalize<kGlassFast>(p - V3{sh.center[0], sh.center[1], sh.center[2]}));
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) pcg_skip3(ps.rng);
     const float qrr = smin(ps.beta.x, 0.99f);
     if (next1D(ps.rng) > qrr) return false;
     ps.beta = ps.beta / qrr;  // (times the sample weight 1, exactly)
-    const V3 wo = dielectric_wo(B, to_local(f, -ps.d), next2D(ps.rng));
+    const V3 wo = dielectric_wo<kGlassFast>(B, to_local(f, -ps.d), next2D(ps.rng));
     if (INTEG == NORI_INTEGRATOR_PATH_MIS) ps.prev = -1.0f;  // discrete measure
     ps.o = p;
     ps.d = to_world(f, wo);
@@ -1994,6 +1999,7 @@ ND bool coop_scan(const DevScene &S, const CoopPrim &cp, const TRay &mine, bool 
 // passes (the ball lies inside the scene box by a margin).  Same arithmetic
 // as the scan's sphere test (sphere_hit_nb, the adaptive epsilon of
 // bvh.cpp:412-418), so t is the scan's; false: the caller scans as usual.
+template <bool FAST = false>
 ND bool chord_hit(const DevShape &sh, const PathState &ps, float &t) {
     TRay r;
     r.o = ps.o;
@@ -2002,8 +2008,8 @@ ND bool chord_hit(const DevShape &sh, const PathState &ps, float &t) {
     r.maxt = ps.maxt;
     if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
     if (r.maxt < r.mint) return false;
-    return sphere_hit_nb(make_float4(sh.center[0], sh.center[1], sh.center[2], 0.0f),
-                         make_float4(sh.radius, 0.0f, 0.0f, 0.0f), r, t);
+    return sphere_hit_nb<FAST>(make_float4(sh.center[0], sh.center[1], sh.center[2], 0.0f),
+                               make_float4(sh.radius, 0.0f, 0.0f, 0.0f), r, t);
 }
 
 // At most this many tracing lanes use the cooperative scan (each costs one
@@ -2165,7 +2171,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
                     shaded = true;
                     if (!alive) break;
                     float tc;
-                    if (!chord_hit(gs, ps, tc)) {
+                    if (!chord_hit<kGlassFast>(gs, ps, tc)) {
                         sol = -1;  // it leaves the sphere: traced below
                         break;
                     }
