@@ -866,6 +866,49 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
+// The BVH walks over a sorted queue order (raysort.hip): entry i of the launch
+// traces the ray in slot order[i].  The grid covers every slot of the part;
+// work-groups past the first ceil(n / kTraceBlock) exit at once, and the busy
+// ones are spread over the XCDs with xcd_block over that count, so each XCD
+// takes a contiguous range of the sorted rays.
+template <int STACK>
+__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_extend_sorted(DevScene S, PathQueue pq,
+                                                                               const uint32_t *order,
+                                                                               const uint32_t *n_ptr) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
+    const uint32_t n = *n_ptr, nb = (n + kTraceBlock - 1) / kTraceBlock;
+    if (blockIdx.x >= nb) return;
+    const uint32_t i = xcd_block(blockIdx.x, nb) * kTraceBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t q = order[i];
+    TRay r;
+    path_ray(S, pq.ray_o[q], pq.ray_d[q], r);
+    float t, u, v;
+    uint32_t p;
+    traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
+    pq.hit[q] = make_float4(t, __uint_as_float(p), u, v);
+}
+template <int STACK>
+__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow_sorted(DevScene S, ShadowQueue sq,
+                                                                               const uint32_t *order,
+                                                                               const uint32_t *n_ptr, float4 *rec) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
+    const uint32_t n = *n_ptr, nb = (n + kTraceBlock - 1) / kTraceBlock;
+    if (blockIdx.x >= nb) return;
+    const uint32_t i = xcd_block(blockIdx.x, nb) * kTraceBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t q = order[i];
+    const float4 a = sq.ray_o[q], b = sq.ray_d[q];
+    TRay r;
+    r.o = ld3(a);
+    r.d = ld3(b);
+    r.mint = a.w;
+    r.maxt = b.w;
+    float t, u, v;
+    uint32_t p;
+    if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) shadow_add(rec, sq.payload[q]);
+}
+
 // Scan-mode traversal of K rays per thread: every primitive record is
 // fetched once (scalar loads) and tested against K independent rays, which
 // gives the VALU K independent dependency chains to interleave.  Results are
@@ -2806,6 +2849,31 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec, G); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_extend_sorted(const DevScene &S, const PathQueue &q, const uint32_t *order, const uint32_t *n,
+                                uint32_t slots, int stack, hipStream_t st) {
+    const dim3 g((slots + kTraceBlock - 1) / kTraceBlock), b(kTraceBlock);
+    switch (stack) {
+    case 8: hipLaunchKernelGGL(k_extend_sorted<8>, g, b, 0, st, S, q, order, n); break;
+    case 16: hipLaunchKernelGGL(k_extend_sorted<16>, g, b, 0, st, S, q, order, n); break;
+    case 32: hipLaunchKernelGGL(k_extend_sorted<32>, g, b, 0, st, S, q, order, n); break;
+    case 64: hipLaunchKernelGGL(k_extend_sorted<64>, g, b, 0, st, S, q, order, n); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_shadow_sorted(const DevScene &S, const ShadowQueue &sq, const uint32_t *order, const uint32_t *n,
+                                float4 *rec, uint32_t slots, int stack, hipStream_t st) {
+    const dim3 g((slots + kTraceBlock - 1) / kTraceBlock), b(kTraceBlock);
+    switch (stack) {
+    case 8: hipLaunchKernelGGL(k_shadow_sorted<8>, g, b, 0, st, S, sq, order, n, rec); break;
+    case 16: hipLaunchKernelGGL(k_shadow_sorted<16>, g, b, 0, st, S, sq, order, n, rec); break;
+    case 32: hipLaunchKernelGGL(k_shadow_sorted<32>, g, b, 0, st, S, sq, order, n, rec); break;
+    case 64: hipLaunchKernelGGL(k_shadow_sorted<64>, g, b, 0, st, S, sq, order, n, rec); break;
+    default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

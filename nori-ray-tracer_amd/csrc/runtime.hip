@@ -204,6 +204,8 @@ struct nori_gpu_ctx {
     // render state
     DevBuf q[2][5], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
     DevBuf ptctr;                    // persistent traversal work counters, 4 per part
+    DevBuf rsort[5];                 // ray reordering (raysort.hip): keys x2, slots x2 (pool each), sort scratch per part
+    DevBuf rsort_n;                  // ... and the ray count of each part's sorted launch
     DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
     DevBuf ph, ph_rgbe, ph_tab, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
     uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
@@ -832,6 +834,13 @@ uint64_t lookahead(const char *name, int dflt) {
     const long v = e ? std::atol(e) : dflt;
     return v >= 1 && v <= kRing - 2 ? (uint64_t)v : (uint64_t)dflt;
 }
+// NORI_RAY_SORT: bits per axis of the origin Morton code that orders the BVH
+// walks of each launch (raysort.hip); 0 = queue order.
+int ray_sort_bits() {
+    const char *e = std::getenv("NORI_RAY_SORT");
+    const long v = e ? std::atol(e) : 0;
+    return v >= 0 && v <= 9 ? (int)v : 0;
+}
 bool fused_extend() {
     const char *e = std::getenv("NORI_FUSED_EXTEND");
     return e && e[0] == '1';
@@ -1181,6 +1190,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // NORI_FUSED_EXTEND=1: scan-mode scenes trace the extension rays inside
     // the shade kernel (measured even with separate k_extend launches)
     const bool fused = c.stack == 0 && fused_extend();
+    const int rsort_bits = c.stack != 0 && !c.pt_grid[0] ? ray_sort_bits() : 0;
     const uint64_t every = event_every(), ahead = lookahead("NORI_LOOKAHEAD", kLookahead),
                    ahead_end = lookahead("NORI_LOOKAHEAD_END", kLookaheadEnd);
     const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(c.stack != 0), pool / kSeg));
@@ -1220,6 +1230,23 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         std::vector<ShadowQueue> sqh(parts);
         std::vector<SegState> segh(parts);
         std::vector<WorkDesc> wdh(parts);
+        // ray reordering of the BVH walks: per part, a window of the key /
+        // slot buffers (slot indices are part-local) and its own scratch
+        std::vector<RaySortBufs> rsb(parts);
+        if (rsort_bits) {
+            uint32_t gmax = 0;
+            for (uint32_t h = 0; h < parts; ++h) gmax = std::max(gmax, Gp[h]);
+            const size_t tb = (ray_sort_temp_bytes(gmax * kSeg, rsort_bits) + 255) / 256 * 256;
+            for (int k = 0; k < 4; ++k) c.rsort[k].ensure(4 * (size_t)pool);
+            c.rsort[4].ensure(tb * parts);
+            c.rsort_n.ensure(4 * kMaxParts);
+            for (uint32_t h = 0; h < parts; ++h) {
+                const size_t e = (size_t)base[h] * kSeg;
+                rsb[h] = RaySortBufs{{c.rsort[0].as<uint32_t>() + e, c.rsort[1].as<uint32_t>() + e},
+                                     {c.rsort[2].as<uint32_t>() + e, c.rsort[3].as<uint32_t>() + e},
+                                     c.rsort[4].as<char>() + tb * h, tb, c.rsort_n.as<uint32_t>() + h};
+            }
+        }
         for (uint32_t h = 0; h < parts; ++h) {
             Qh[h][0] = q_view(Q[0], base[h]);
             Qh[h][1] = q_view(Q[1], base[h]);
@@ -1250,6 +1277,25 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                     for (uint32_t k = 1; k < parts; ++k) HIP_TRY(hipStreamWaitEvent(c.parts[k], c.fork, 0));
                 }
                 uint32_t *ctr = c.pt_grid[0] ? c.ptctr.as<uint32_t>() + 4 * h : nullptr;
+                if (rsort_bits) {
+                    const RaySortBufs &R = rsb[h];
+                    const uint32_t slots = Gp[h] * kSeg;
+                    // the sorts' time is counted with the walks they order
+                    timed_on(st, 0, [&] {
+                        return launch_ray_sort(S, Qh[h][out].ray_o, Qh[h][out].ray_d, sg.cnt[out], Gp[h], rsort_bits,
+                                               R, st);
+                    });
+                    timed_on(st, 0, [&] {
+                        return launch_extend_sorted(S, Qh[h][out], R.vals[1], R.n, slots, c.stack, st);
+                    });
+                    timed_on(st, 1, [&] {
+                        return launch_ray_sort(S, sqh[h].ray_o, sqh[h].ray_d, sg.shcnt, Gp[h], rsort_bits, R, st);
+                    });
+                    timed_on(st, 1, [&] {
+                        return launch_shadow_sorted(S, sqh[h], R.vals[1], R.n, c.rec.as<float4>(), slots, c.stack, st);
+                    });
+                    continue;
+                }
                 if (!fused)
                     timed_on(st, 0, [&] {
                         return ctr ? launch_extend_pt(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, ctr, c.pt_grid[0], st)
