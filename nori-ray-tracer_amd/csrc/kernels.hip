@@ -2209,6 +2209,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
             const DevShape &gs = S.shapes[sol];
             const DevBsdf &gb = S.bsdfs[gs.bsdf];
             if (gb.type == NORI_BSDF_DIELECTRIC && gs.emitter < 0) {
+#ifdef NORI_PROF_GLASS  // diagnostic build: wall time of lone-lane chains per chord bounce
+                const bool lone = __popcll(__ballot(active)) == 1;
+                const uint64_t g0 = __builtin_amdgcn_s_memrealtime();
+                const uint32_t r0 = rays;
+#endif
                 while (INTEG != NORI_INTEGRATOR_PATH_MIS || skip_nee(S, gb, ps.beta)) {
                     alive = glass_bounce<INTEG>(gs, gb, ps, h.x);
                     shaded = true;
@@ -2222,6 +2227,12 @@ __global__ __launch_bounds__(kTraceBlock) void k_finish(DevScene Sg, PathQueue Q
                     ++rays;
                     shaded = false;
                 }
+#ifdef NORI_PROF_GLASS
+                if (lone && rays - r0 >= 8) {
+                    atomicAdd(&C->prof[13], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - g0));
+                    atomicAdd(&C->prof[14], (unsigned long long)(rays - r0));
+                }
+#endif
             }
         }
         if (active && !shaded) alive = shade_vertex<INTEG, false, FULL>(S, ps, h, rec, so);

@@ -1398,6 +1398,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                              (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4],
                              (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4],
                              (double)(hc.prof[5] >> 20) * 1e-5, hc.prof[5] & 0xFFFFFull);
+            if (hc.prof[14])  // NORI_PROF_GLASS builds
+                std::fprintf(stderr, "[nori] lone-lane glass chains: %llu chord bounces, %.0f ns each\n", hc.prof[14],
+                             10.0 * hc.prof[13] / hc.prof[14]);
             if (hc.prof[12])
                 std::fprintf(stderr, "[nori] finisher late iterations (lone lanes): shade %.0f shadow %.0f splat %.0f extend %.0f ns (%llu)\n",
                              10.0 * hc.prof[8] / hc.prof[12], 10.0 * hc.prof[9] / hc.prof[12],

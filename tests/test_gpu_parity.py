@@ -210,3 +210,18 @@ def test_render_modes_agree(built, mode):
     r.close()
     cpu = nori_amd.develop(s, pyoracle.OracleScene(s).render(rng="wave"))
     assert_parity(image_parity(gpu, cpu))
+
+
+@pytest.mark.parametrize("bits", ["3", "5"])
+def test_ray_sort_same_image(hfield, bits):
+    """NORI_RAY_SORT (raysort.hip, opt-in): the BVH walks in Morton-sorted
+    order give every ray the same hit, so the film is the unsorted one up to
+    the film sums' order."""
+    s, r, o = hfield
+    base = r.render()
+    os.environ["NORI_RAY_SORT"] = bits
+    try:
+        srt = r.render()
+    finally:
+        os.environ.pop("NORI_RAY_SORT", None)
+    assert np.allclose(base, srt, rtol=1e-5, atol=1e-6), np.abs(base - srt).max()
