@@ -87,6 +87,22 @@ ND float rcp_rn(float x) {
 #endif
 }
 
+// 1.0f / x for every float x: rcp_rn inside the verified range, the IEEE
+// division outside it (zero, denormals, |x| > 2^125, inf, NaN) -- so the
+// result is always the IEEE quotient.  Used where x may be zero (ray
+// direction components: the slab test's d_i == 0 case, bbox.h:344-346).
+NHD float rcp_full(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const float a = __builtin_fabsf(x);
+    if (__builtin_expect(!(a >= 0x1p-125f && a <= 0x1p125f), 0)) return 1.0f / x;
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+#else
+    return 1.0f / x;
+#endif
+}
+
 // ---------------------------------------------------------------- pcg32
 // ext/pcg32/pcg32.h:51-110.  The increment of a WAVE stream is derived from
 // its sample id, so a path only carries the 64-bit state.
@@ -154,10 +170,10 @@ NHD Frame frame_from(V3 a) {  // frame.h:49-51 + coordinateSystem common.cpp:274
     Frame f;
     f.n = a;
     if (fabsf(a.x) > fabsf(a.y)) {
-        float invLen = 1.0f / fsqrt<FAST>(a.x * a.x + a.z * a.z);
+        float invLen = rcp_full(fsqrt<FAST>(a.x * a.x + a.z * a.z));
         f.t = V3{a.z * invLen, 0.0f, -a.x * invLen};
     } else {
-        float invLen = 1.0f / fsqrt<FAST>(a.y * a.y + a.z * a.z);
+        float invLen = rcp_full(fsqrt<FAST>(a.y * a.y + a.z * a.z));
         f.t = V3{0.0f, a.z * invLen, -a.y * invLen};
     }
     f.s = cross(f.t, a);

@@ -201,7 +201,7 @@ ND void scan_prologue(const DevScene &S, TRay (&r)[K], bool (&live)[K]) {
     for (int k = 0; k < K; ++k) {
         TRay &x = r[k];
         if (x.mint == kEps) x.mint = smax(x.mint, x.mint * smax(smax(fabsf(x.o.x), fabsf(x.o.y)), fabsf(x.o.z)));
-        x.rcp = V3{1.0f / x.d.x, 1.0f / x.d.y, 1.0f / x.d.z};
+        x.rcp = V3{rcp_full(x.d.x), rcp_full(x.d.y), rcp_full(x.d.z)};
         float tn;
         live[k] = live[k] && !(x.maxt < x.mint) && box_test(rmn, rmx, x, tn);
     }
@@ -311,7 +311,7 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     tb = INF_F;
     pb = 0xFFFFFFFFu;
     ub = vb = 0.0f;
-    r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    r.rcp = V3{rcp_full(r.d.x), rcp_full(r.d.y), rcp_full(r.d.z)};
     if (r.maxt < r.mint) return false;
     // 4-wide nodes: test the four child boxes, enter the nearest hit child and
     // push the others farthest first.  Box tests are monotone (a child box lies
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(Dev
                         path_ray(S, a, b, r);
                     }
                     if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
-                    r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+                    r.rcp = V3{rcp_full(r.d.x), rcp_full(r.d.y), rcp_full(r.d.z)};
                     tb = INF_F;
                     pb = 0xFFFFFFFFu;
                     ub = vb = 0.0f;
@@ -1997,7 +1997,7 @@ ND bool coop_scan(const DevScene &S, const CoopPrim &cp, const TRay &mine, bool 
         r.mint = bcast(mine.mint, j);
         r.maxt = bcast(mine.maxt, j);
         if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
-        r.rcp = V3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+        r.rcp = V3{rcp_full(r.d.x), rcp_full(r.d.y), rcp_full(r.d.z)};
         float tn;
         const bool live = !(r.maxt < r.mint) && box_test(rmn, rmx, r, tn);
         float tl = 0, ul = 0, vl = 0;
