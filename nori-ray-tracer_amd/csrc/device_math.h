@@ -346,7 +346,7 @@ ND float smith_G1(const DevBsdf &b, V3 v, V3 m) {  // microfacet.cpp:56-76
     float tanTheta = tan_theta(v);
     if (tanTheta == 0.0f) return 1.0f;
     if (dot(m, v) * v.z <= 0) return 0.0f;
-    float a = 1.0f / (b.alpha * tanTheta);
+    float a = rcp_full(b.alpha * tanTheta);
     if (a >= 1.6f) return 1.0f;
     float a2 = a * a;
     return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
@@ -358,7 +358,7 @@ ND float schlick(float u) {  // disney.cpp:25-29: pow(m, 5) in double
 }
 ND float ggx(float NdotV, float alphaG) {  // disney.cpp:31-36
     float a = alphaG * alphaG, b = NdotV * NdotV;
-    return 1 / (NdotV + sqrtf(a + b - a * b));
+    return rcp_full(NdotV + sqrtf(a + b - a * b));
 }
 ND V3 lerp3(float t, V3 a, V3 c) { return a * (1.0f - t) + c * t; }  // disney.cpp:40-42
 

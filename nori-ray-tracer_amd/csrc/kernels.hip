@@ -1191,7 +1191,7 @@ ND void camera_sample(const DevScene &S, float px, float py, V2 ap, int channel,
         chroma = S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f;
         if (chroma) w = S.chromatic[channel < 0 ? 0 : (channel > 2 ? 2 : channel)];
     }
-    const float invZ = 1.0f / dl.z;
+    const float invZ = rcp_full(dl.z);
     const float *c = S.c2w;
     V3 lo = V3{0, 0, 0};
     if (FULL && S.cam_type != NORI_CAMERA_PERSPECTIVE && (S.lens_radius > 0.0f || chroma)) {
@@ -1289,7 +1289,7 @@ ND bool mbox_range(const DevScene &S, V3 o, V3 d, float &nearT, float &farT) {
         if (dc[i] == 0.0f) {
             if (origin < mn || origin > mx) return false;
         } else {
-            const float r = 1.0f / dc[i];
+            const float r = rcp_full(dc[i]);
             float t1 = (mn - origin) * r, t2 = (mx - origin) * r;
             if (t1 > t2) {
                 float t = t1;
