@@ -2094,7 +2094,10 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #define NORI_FINISH_PRIO 1
 #endif
 #ifndef NORI_FINISH_WAVES  // 0: 64 paths per wave
-#define NORI_FINISH_WAVES 8192
+// 2048 since the glass-sphere chain (round 3): fewer finisher waves leave the
+// film splat beside it more of the chip; 64-spp share 3446 -> 3550 (4096) ->
+// 3652 (2048) Msamples/s, 512 spp 4737 -> 4753 / 4744 (one box, interleaved)
+#define NORI_FINISH_WAVES 2048
 #endif
 constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
 #ifndef NORI_FINISH_GLASS  // 0: the tail finisher shades glass-sphere vertices generically
