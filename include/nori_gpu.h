@@ -385,14 +385,27 @@ int nori_gpu_shard_desc(const nori_scene_desc *scene, const nori_gpu_render_desc
  * be NULL (per-pixel statistics are not summed across ranks).
  * Failure handling: every rank joins a status exchange before the film sum.
  * If any rank's share was cancelled (nori_gpu_cancel) every rank returns
- * NORI_ERR_CANCELLED; if any failed, the failing rank returns its error and
- * the others NORI_ERR_INVALID ("the frame is incomplete"); no film sum runs.
- * A HIP error, an RCCL error, or peers that do not reach the collective within
- * NORI_COMM_TIMEOUT_S seconds (default 600) abort the communicator
- * (ncclCommAbort) and return NORI_ERR_HIP; an aborted communicator fails every
- * later call. */
+ * NORI_ERR_CANCELLED; if any failed (bad arguments, allocation, a HIP error
+ * that leaves the device usable, any exception of the render), the failing
+ * rank returns its error and the others NORI_ERR_INVALID ("the frame is
+ * incomplete"); no film sum runs and the communicator stays usable.  A rank
+ * whose device faulted (a sticky HIP error) cannot join: it aborts the
+ * communicator (ncclCommAbort) and returns NORI_ERR_HIP.  Its peers, and any
+ * rank whose peers do not reach a collective, give up after the watchdog
+ * bound nori_gpu_comm_timeout(own render seconds, own samples, largest
+ * share's samples) -- max(30 s, 20 x the own render time scaled to the
+ * largest share), 600 s for a rank without a share, NORI_COMM_TIMEOUT_S
+ * seconds if set -- abort and return NORI_ERR_HIP; an aborted communicator
+ * fails every later call. */
 int nori_gpu_render_sharded(nori_gpu_ctx *ctx, nori_gpu_comm *comm, const nori_gpu_render_desc *desc, int mode,
                             int root, float *film_dev, nori_gpu_stats *stats);
+/* The status word a rank contributes to the exchange (reduced by max):
+ * severity << 16 | rank, severity 0 for NORI_OK, 1 for NORI_ERR_CANCELLED,
+ * 2 for any other status.  Pure function. */
+int nori_gpu_comm_status_word(int status, int rank);
+/* The watchdog bound of a sharded render's collectives, in seconds (see
+ * nori_gpu_render_sharded).  Pure function (reads NORI_COMM_TIMEOUT_S). */
+double nori_gpu_comm_timeout(double own_seconds, double own_samples, double max_samples);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,10 @@ struct DevScene {
     uint32_t num_nodes;
     uint32_t num_prims;
     uint32_t num_scan_tris;  // scan mode: prims = triangles (padded to kScanGroup), then spheres
+    // scan mode: triangle filter groups (runtime.hip build_scan_groups), two
+    // float4 each: (min.xyz, scan-index mask bits 0-31) (max.xyz, bits 32-63)
+    const float4 *scan_boxes;
+    uint32_t num_scan_boxes;
     float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;
     float invW, invH;

@@ -46,10 +46,8 @@ struct SplatDesc {
 // stack = LDS stack depth (8, 16, 32 or 64) chosen from the BVH depth.
 hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int any_hit, float4 *hits, int stack,
                         hipStream_t st);
-// trace: also find the closest hit of every outgoing ray (scan-mode scenes;
-// launch_extend is then skipped).
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
+                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                         uint32_t nseg, hipStream_t st);
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st);
@@ -64,33 +62,6 @@ hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                          hipStream_t st);
-// Persistent BVH traversal (k_trace_pt): `blocks` resident work-groups pull
-// queue segments through ctr[0..1] (zero before the first launch; each launch
-// leaves them zero).  Stacks 8, 16, 32 only (BVH scenes).
-hipError_t launch_extend_pt(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
-                            uint32_t *ctr, uint32_t blocks, hipStream_t st);
-hipError_t launch_shadow_pt(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
-                            int stack, uint32_t *ctr, uint32_t blocks, hipStream_t st);
-int pt_blocks_per_cu(int stack, bool any);
-// Queue-wide ray reordering of the BVH walks (raysort.hip): the G*kSeg slots
-// of a part's queue are keyed (origin Morton code, `bits` per axis, and the
-// direction octant; empty slots last) and sorted; vals[1] then holds the
-// slots in traversal order and *n the number of rays.
-struct RaySortBufs {
-    uint32_t *keys[2], *vals[2];
-    void *temp;
-    size_t temp_bytes;
-    uint32_t *n;
-};
-size_t ray_sort_temp_bytes(uint32_t slots, int bits);
-hipError_t launch_ray_sort(const DevScene &S, const float4 *ro, const float4 *rd, const uint32_t *cnt, uint32_t G,
-                           int bits, const RaySortBufs &B, hipStream_t st);
-// The BVH walks over a sorted order: `slots` queue slots at most, the first *n
-// entries of `order` traced (same results as launch_extend / launch_shadow).
-hipError_t launch_extend_sorted(const DevScene &S, const PathQueue &q, const uint32_t *order, const uint32_t *n,
-                                uint32_t slots, int stack, hipStream_t st);
-hipError_t launch_shadow_sorted(const DevScene &S, const ShadowQueue &sq, const uint32_t *order, const uint32_t *n,
-                                float4 *rec, uint32_t slots, int stack, hipStream_t st);
 // Photon tracing (photonmapper preprocess): count pass (out == null) writes
 // the photons stored by each emitted photon e0 + i into count[i]; store pass
 // writes the photons of emitted photons i < n at pre[i] (3 float4 each:

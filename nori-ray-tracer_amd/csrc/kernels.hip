@@ -268,6 +268,136 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
     }
 }
 
+// BoundingBox3f::rayIntersect for a ray whose three reciprocals are finite
+// and non-zero: no slab is NaN unless the origin is, so the swap / max / min
+// steps of bbox.h:336-363 are the plain min and max below and the result is
+// the reference's (a NaN origin, which the reference rejects, may pass here:
+// this is only used to skip work, never to accept a hit).
+ND bool box_lean(const float4 &mn, const float4 &mx, const TRay &r) {
+    const float x1 = (mn.x - r.o.x) * r.rcp.x, x2 = (mx.x - r.o.x) * r.rcp.x;
+    const float y1 = (mn.y - r.o.y) * r.rcp.y, y2 = (mx.y - r.o.y) * r.rcp.y;
+    const float z1 = (mn.z - r.o.z) * r.rcp.z, z2 = (mx.z - r.o.z) * r.rcp.z;
+    const float nearT = fmaxf(fmaxf(fminf(x1, x2), fminf(y1, y2)), fminf(z1, z2));
+    const float farT = fminf(fminf(fmaxf(x1, x2), fmaxf(y1, y2)), fmaxf(z1, z2));
+    return nearT <= farT && r.mint <= farT && nearT <= r.maxt;
+}
+
+// Box-filtered scan of the scan-mode trace kernels (k_extend_scan,
+// k_shadow_scan).  The reference tests a primitive only after the ray has
+// passed the box of the BVH leaf that holds it (bvh.cpp:420-443), with the
+// current maxt, which never exceeds the ray's own.  Slab tests are monotone in
+// the box and in maxt (every step of bbox.h:336-363 rounds monotonically), so
+// a ray that misses a box B containing the leaf box of p, tested with its own
+// [mint, maxt], is never tested against p by the reference, whatever the
+// order of its traversal.  The host pairs the scan's triangles into groups
+// (runtime.hip build_scan_groups) whose B is the union of the members' leaf
+// boxes.  Each lane first tests its ray against every group box (scalar loads,
+// shared by the K rays) and collects the scan indices of the groups it
+// passes; it then runs the exact triangle test on those candidates only, in
+// scan order -- its own loop, so a lane pays for its 1-4 candidates instead
+// of the whole list -- and the spheres by the wave-uniform scan.  Closest hit
+// and ties (the last primitive in scan order wins) are those of scan_core over
+// the candidates, and a triangle left out is one the reference never tests.
+template <int K, bool ANY>
+ND void scan_filtered(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
+                      float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
+    scan_prologue<K>(S, r, live);
+    bool lean = true;  // every live ray's reciprocals finite (no zero direction component)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        tb[k] = INF_F;
+        pb[k] = 0xFFFFFFFFu;
+        ub[k] = vb[k] = 0.0f;
+        found[k] = false;
+        lean = lean && (!live[k] || (fabsf(r[k].rcp.x) < INF_F && fabsf(r[k].rcp.y) < INF_F && fabsf(r[k].rcp.z) < INF_F));
+    }
+    uint64_t cand[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cand[k] = 0;
+    const uint32_t ng = S.num_scan_boxes;
+    auto collect = [&](auto test) {
+        for (uint32_t g = 0; g < ng; ++g) {
+            const float4 mn = S.scan_boxes[2 * g], mx = S.scan_boxes[2 * g + 1];
+            const uint64_t gm = (uint64_t)__float_as_uint(mx.w) << 32 | __float_as_uint(mn.w);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (live[k] && test(mn, mx, r[k])) cand[k] |= gm;
+        }
+    };
+    if (__all(lean)) {
+        collect([](const float4 &mn, const float4 &mx, const TRay &x) { return box_lean(mn, mx, x); });
+    } else {
+        collect([](const float4 &mn, const float4 &mx, const TRay &x) {
+            float tn;
+            return box_test(mn, mx, x, tn);
+        });
+    }
+    // the candidates, lowest scan index first (per lane: divergent loop)
+    for (;;) {
+        bool more = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) more = more || cand[k] != 0;
+        if (!more) break;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (cand[k] == 0) continue;
+            const uint32_t i = (uint32_t)__builtin_ctzll(cand[k]);
+            cand[k] &= cand[k] - 1;
+            // (plain loads: the tail finisher and the shade kernel pass a
+            // scene whose tables are staged in LDS)
+            const float4 *p = S.prims + 3 * (size_t)i;
+            const float4 a = p[0];
+            float t, u, v;
+            if (tri_hit(a, p[1], p[2], r[k], t, u, v)) {
+                found[k] = true;
+                if (ANY) {
+                    cand[k] = 0;
+                } else {
+                    r[k].maxt = tb[k] = t;
+                    ub[k] = u;
+                    vb[k] = v;
+                    pb[k] = __float_as_uint(a.w);
+                }
+            }
+        }
+    }
+    auto all_done = [&]() {
+        bool done = true;
+#pragma unroll
+        for (int k = 0; k < K; ++k) done = done && (found[k] || !live[k]);
+        return __all(done);
+    };
+    for (uint32_t i = S.num_scan_tris, n = S.num_prims; i < n; ++i) {
+        if (ANY && all_done()) return;
+        const float4 *p = S.prims + 3 * (size_t)i;
+        const float4 p0 = p[0], p1 = p[1];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float t = 0;
+            const bool h = sphere_hit_nb(p0, p1, r[k], t);
+            if (h && live[k]) {
+                found[k] = true;
+                if (!ANY) {
+                    r[k].maxt = tb[k] = t;
+                    ub[k] = vb[k] = 0.0f;
+                    pb[k] = __float_as_uint(p0.w);
+                }
+            }
+        }
+    }
+}
+
+// Scan-mode traversal of K rays per thread: every primitive record is
+// fetched once (scalar loads) and tested against K independent rays, which
+// gives the VALU K independent dependency chains to interleave.  Results are
+// those of traverse<0, ANY> ray by ray.
+template <int K, bool ANY>
+ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
+                  float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
+    if (S.num_scan_boxes) scan_filtered<K, ANY>(S, r, live, tb, pb, ub, vb, found);
+    else scan_core<K, ANY>(S, r, live, tb, pb, ub, vb, found);
+}
+
 // Primitive records fetched per memory round trip in a BVH leaf.
 #ifndef NORI_LEAF_BATCH
 #define NORI_LEAF_BATCH 1
@@ -300,7 +430,7 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
         bool live[1] = {true}, found[1];
         float t1[1], u1[1], v1[1];
         uint32_t p1[1];
-        scan_core<1, ANY>(S, rr, live, t1, p1, u1, v1, found);
+        scan_rays<1, ANY>(S, rr, live, t1, p1, u1, v1, found);
         tb = t1[0];
         pb = p1[0];
         ub = u1[0];
@@ -552,23 +682,12 @@ ND void extend_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt,
 // path_mis.cpp:48-60).  A record belongs to one path, which has at most one
 // shadow ray per launch, so a plain read-modify-write is race free; it runs
 // after the traversal, for unoccluded rays only (reading every ray's record
-// before the scan fetched 2.3x the algorithmic bytes).  NORI_SHADOW_ATOMIC=1:
-// three returnless float atomics instead (same IEEE sums; measured 1.8x
-// slower on cbox: every atomic writes its line through).
-#ifndef NORI_SHADOW_ATOMIC
-#define NORI_SHADOW_ATOMIC 0
-#endif
+// before the scan fetched 2.3x the algorithmic bytes; three returnless float
+// atomics measured 1.8x slower on cbox: every atomic writes its line through).
 ND void shadow_add(float4 *rec, const float4 &c) {
-#if NORI_SHADOW_ATOMIC
-    float *r = reinterpret_cast<float *>(rec + __float_as_uint(c.w));
-    atomicAdd(r + 0, c.x);
-    atomicAdd(r + 1, c.y);
-    atomicAdd(r + 2, c.z);
-#else
     const uint32_t w = __float_as_uint(c.w);
     const float4 L = rec[w];
     rec[w] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
-#endif
 }
 
 // Shadow rays: any hit; unoccluded -> record += payload.
@@ -588,251 +707,6 @@ ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *sh
         float t, u, v;
         uint32_t p;
         if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) shadow_add(rec, sq.payload[q]);
-    }
-}
-
-// ------------------------------------------------------------------ persistent traversal
-// BVH scenes: incoherent rays make a one-ray-per-thread wave run as long as
-// its longest ray (measured on C3: ~13 node/leaf rounds per wave for ~5 per
-// ray).  The persistent kernels below keep a fixed set of waves resident:
-//  * dynamic fetch -- a wave owns one queue segment at a time (claimed with
-//    one atomic per segment) and hands its next entries to idle lanes
-//    whenever at least kRefill lanes are idle, so lanes do not idle until the
-//    wave's longest ray ends (Aila & Laine 2009, "persistent while-while");
-//  * while-while with postponed leaves -- the node loop runs until every
-//    busy lane holds a leaf, then the leaf loop intersects them together, so
-//    node and leaf code do not alternate inside a diverged wave.
-// The candidate primitives of a ray are those of traverse() (same box test,
-// same key culling against the current closest t), so t and the hit are the
-// same; only the order among equal-t primitives may differ.
-// ctr[0]: next segment, ctr[1]: retired waves; the last wave to retire
-// resets both, so the next launch starts from zero without a memset.
-#ifndef NORI_PT_REFILL
-#define NORI_PT_REFILL 16
-#endif
-constexpr int kRefill = NORI_PT_REFILL;
-#ifndef NORI_PT_SPEC  // 1: postpone leaves until every busy lane holds one; 0: intersect as soon as one does
-#define NORI_PT_SPEC 1
-#endif
-#ifdef NORI_PT_WAVES
-#define NORI_TRACE_ATTR_PT __attribute__((amdgpu_waves_per_eu(NORI_PT_WAVES)))
-#else
-#define NORI_TRACE_ATTR_PT
-#endif
-
-template <bool ANY>
-struct PtJob {
-    const float4 *ray_o, *ray_d;
-    float4 *hit;            // closest hit (extension rays)
-    const float4 *payload;  // shadow rays: contribution, work id in w
-    float4 *rec;            // shadow rays: sample records
-};
-
-template <int STACK, bool ANY>
-__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR_PT void k_trace_pt(DevScene S, PtJob<ANY> J,
-                                                                             const uint32_t *cnt, uint32_t G,
-                                                                             uint32_t *ctr) {
-    __shared__ uint32_t stk_lds[stack_words(STACK) * kTraceBlock];
-    uint32_t *stk = stk_lds + threadIdx.x;
-    constexpr int L = stack_lds_entries(STACK);
-    uint32_t spill[kTraceSpill];
-    float spillk[kTraceSpill];
-    const uint32_t lane = lane_id();
-    // wave-uniform work cursor: current segment, its count, next entry
-    uint32_t seg = 0, seg_n = 0, seg_pos = 0;
-    bool have_seg = false;  // becomes false for good once the segments run out
-    bool more = true;
-    // lane state
-    bool active = false, has_ref = false, has_leaf = false, found = false;
-    uint32_t q = 0, ref = 0, leaf = 0, pb = 0xFFFFFFFFu;
-    int sp = 0;
-    TRay r;
-    r.o = r.d = r.rcp = V3{0, 0, 0};
-    r.mint = r.maxt = 0.0f;
-    float tb = INF_F, ub = 0.0f, vb = 0.0f;
-    auto push = [&](uint32_t v, float k) {
-        if (sp < L) {
-            stk[sp * kTraceBlock] = v;
-            stk[(L + sp) * kTraceBlock] = __float_as_uint(k);
-        } else {
-            spill[sp - L] = v;
-            spillk[sp - L] = k;
-        }
-        ++sp;
-    };
-    // next stack entry whose box starts within the current closest hit
-    auto pop = [&]() -> bool {
-        while (sp > 0) {
-            --sp;
-            const uint32_t v = sp < L ? stk[sp * kTraceBlock] : spill[sp - L];
-            const float key = sp < L ? __uint_as_float(stk[(L + sp) * kTraceBlock]) : spillk[sp - L];
-            if (!(key > r.maxt)) {
-                ref = v;
-                return true;
-            }
-        }
-        return false;
-    };
-    for (;;) {
-        // ---- refill idle lanes from the wave's segment(s)
-        uint64_t idle = __ballot(!active);
-        if (more && (uint32_t)__popcll(idle) >= (uint32_t)kRefill) {
-            uint32_t need = (uint32_t)__popcll(idle), given = 0;
-            const uint32_t my = rank_in(idle);
-            while (need > 0) {
-                if (!have_seg || seg_pos >= seg_n) {
-                    uint32_t s = 0;
-                    if (lane == 0) s = atomicAdd(&ctr[0], 1u);
-                    s = __builtin_amdgcn_readfirstlane(s);
-                    if (s >= G) {
-                        more = false;
-                        break;
-                    }
-                    seg = s;
-                    seg_n = cnt[s];
-                    seg_pos = 0;
-                    have_seg = true;
-                    continue;
-                }
-                const uint32_t take = min(need, seg_n - seg_pos);
-                if (!active && my >= given && my < given + take) {
-                    q = seg * kSeg + seg_pos + (my - given);
-                    const float4 a = J.ray_o[q], b = J.ray_d[q];
-                    if (ANY) {  // shadow queue: (o, mint), (d, maxt)
-                        r.o = ld3(a);
-                        r.d = ld3(b);
-                        r.mint = a.w;
-                        r.maxt = b.w;
-                    } else {
-                        path_ray(S, a, b, r);
-                    }
-                    if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
-                    r.rcp = V3{rcp_full(r.d.x), rcp_full(r.d.y), rcp_full(r.d.z)};
-                    tb = INF_F;
-                    pb = 0xFFFFFFFFu;
-                    ub = vb = 0.0f;
-                    found = false;
-                    sp = 0;
-                    ref = 0;
-                    has_ref = !(r.maxt < r.mint);
-                    has_leaf = false;
-                    active = true;
-                }
-                given += take;
-                need -= take;
-                seg_pos += take;
-            }
-        }
-        if (!__any(active)) {
-            if (!more) break;
-            continue;
-        }
-        // ---- node loop: descend until every busy lane holds a leaf
-        for (;;) {
-            if (active && has_ref && (ref & 0x80000000u) && !has_leaf) {
-                leaf = ref;
-                has_leaf = true;
-                has_ref = pop();
-            }
-            const bool in_node = active && has_ref && !(ref & 0x80000000u);
-            if (!__any(in_node)) break;
-            if (NORI_PT_SPEC ? __all(!active || has_leaf || !has_ref) : __any(active && has_leaf)) break;
-            if (in_node) {
-                float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
-                load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
-                float k0, k1, k2, k3;
-                const bool h0 = box_test(make_float4(mnx.x, mny.x, mnz.x, 0), make_float4(mxx.x, mxy.x, mxz.x, 0), r, k0);
-                const bool h1 = box_test(make_float4(mnx.y, mny.y, mnz.y, 0), make_float4(mxx.y, mxy.y, mxz.y, 0), r, k1);
-                const bool h2 = box_test(make_float4(mnx.z, mny.z, mnz.z, 0), make_float4(mxx.z, mxy.z, mxz.z, 0), r, k2);
-                const bool h3 = box_test(make_float4(mnx.w, mny.w, mnz.w, 0), make_float4(mxx.w, mxy.w, mxz.w, 0), r, k3);
-                k0 = h0 ? k0 : INF_F;
-                k1 = h1 ? k1 : INF_F;
-                k2 = h2 ? k2 : INF_F;
-                k3 = h3 ? k3 : INF_F;
-                const int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
-                if (nh > 0) {
-                    uint32_t c0 = __float_as_uint(rf.x), c1 = __float_as_uint(rf.y), c2 = __float_as_uint(rf.z),
-                             c3 = __float_as_uint(rf.w);
-                    bool m0 = !h0, m1 = !h1, m2 = !h2, m3 = !h3;
-                    auto cs = [](float &ka, uint32_t &ca, bool &ma, float &kb, uint32_t &cb, bool &mb) {
-                        const bool sw = ma > mb || (ma == mb && kb < ka);
-                        const float tk = ka;
-                        const uint32_t tc = ca;
-                        const bool tm = ma;
-                        ka = sw ? kb : ka;
-                        kb = sw ? tk : kb;
-                        ca = sw ? cb : ca;
-                        cb = sw ? tc : cb;
-                        ma = sw ? mb : ma;
-                        mb = sw ? tm : mb;
-                    };
-                    cs(k0, c0, m0, k1, c1, m1);
-                    cs(k2, c2, m2, k3, c3, m3);
-                    cs(k0, c0, m0, k2, c2, m2);
-                    cs(k1, c1, m1, k3, c3, m3);
-                    cs(k1, c1, m1, k2, c2, m2);
-                    if (nh > 3) push(c3, k3);
-                    if (nh > 2) push(c2, k2);
-                    if (nh > 1) push(c1, k1);
-                    ref = c0;
-                } else {
-                    has_ref = pop();
-                }
-            }
-        }
-        // ---- leaf loop: intersect the postponed leaves (and leaves reached next)
-        for (;;) {
-            const bool lf = active && has_leaf;
-            if (!__any(lf)) break;
-            if (lf) {
-                const uint32_t start = leaf & 0x1FFFFFFu, end = start + ((leaf >> 25) & 63u) + 1u;
-                for (uint32_t i = start; i < end; ++i) {
-                    const float4 *p = S.prims + 3 * (size_t)i;
-                    const float4 p0 = gld(p), p1 = gld(p + 1);
-                    float t = 0, u = 0, v = 0;
-                    bool h;
-                    if (__float_as_uint(p1.w) == 0u) {
-                        const float4 p2 = gld(p + 2);
-                        h = tri_hit(p0, p1, p2, r, t, u, v);
-                    } else {
-                        h = sphere_hit(p0, p1, r, t);
-                        u = v = 0.0f;
-                    }
-                    if (h) {
-                        found = true;
-                        if (ANY) break;
-                        r.maxt = tb = t;
-                        ub = u;
-                        vb = v;
-                        pb = __float_as_uint(p0.w);
-                    }
-                }
-                has_leaf = false;
-                if (ANY && found) has_ref = false;
-                if (has_ref && (ref & 0x80000000u)) {
-                    leaf = ref;
-                    has_leaf = true;
-                    has_ref = pop();
-                }
-            }
-        }
-        // ---- retire finished rays
-        if (active && !has_ref && !has_leaf) {
-            if (ANY) {
-                if (!found) shadow_add(J.rec, J.payload[q]);
-            } else {
-                J.hit[q] = make_float4(tb, __uint_as_float(pb), ub, vb);
-            }
-            active = false;
-        }
-    }
-    // the last wave of the launch to retire resets the work counters
-    if (lane == 0) {
-        const uint32_t waves = gridDim.x * (kTraceBlock / 64);
-        if (atomicAdd(&ctr[1], 1u) == waves - 1) {
-            atomicExch(&ctr[0], 0u);
-            atomicExch(&ctr[1], 0u);
-        }
     }
 }
 
@@ -866,59 +740,6 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
-// The BVH walks over a sorted queue order (raysort.hip): entry i of the launch
-// traces the ray in slot order[i].  The grid covers every slot of the part;
-// work-groups past the first ceil(n / kTraceBlock) exit at once, and the busy
-// ones are spread over the XCDs with xcd_block over that count, so each XCD
-// takes a contiguous range of the sorted rays.
-template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_extend_sorted(DevScene S, PathQueue pq,
-                                                                               const uint32_t *order,
-                                                                               const uint32_t *n_ptr) {
-    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    const uint32_t n = *n_ptr, nb = (n + kTraceBlock - 1) / kTraceBlock;
-    if (blockIdx.x >= nb) return;
-    const uint32_t i = xcd_block(blockIdx.x, nb) * kTraceBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t q = order[i];
-    TRay r;
-    path_ray(S, pq.ray_o[q], pq.ray_d[q], r);
-    float t, u, v;
-    uint32_t p;
-    traverse<STACK, false>(S, r, stk + threadIdx.x, t, p, u, v);
-    pq.hit[q] = make_float4(t, __uint_as_float(p), u, v);
-}
-template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow_sorted(DevScene S, ShadowQueue sq,
-                                                                               const uint32_t *order,
-                                                                               const uint32_t *n_ptr, float4 *rec) {
-    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
-    const uint32_t n = *n_ptr, nb = (n + kTraceBlock - 1) / kTraceBlock;
-    if (blockIdx.x >= nb) return;
-    const uint32_t i = xcd_block(blockIdx.x, nb) * kTraceBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t q = order[i];
-    const float4 a = sq.ray_o[q], b = sq.ray_d[q];
-    TRay r;
-    r.o = ld3(a);
-    r.d = ld3(b);
-    r.mint = a.w;
-    r.maxt = b.w;
-    float t, u, v;
-    uint32_t p;
-    if (!traverse<STACK, true>(S, r, stk + threadIdx.x, t, p, u, v)) shadow_add(rec, sq.payload[q]);
-}
-
-// Scan-mode traversal of K rays per thread: every primitive record is
-// fetched once (scalar loads) and tested against K independent rays, which
-// gives the VALU K independent dependency chains to interleave.  Results are
-// those of traverse<0, ANY> ray by ray.
-template <int K, bool ANY>
-ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
-                  float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
-    scan_core<K, ANY>(S, r, live, tb, pb, ub, vb, found);
-}
-
 template <int K>
 __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
                                                              uint32_t G) {
@@ -1419,9 +1240,6 @@ ND V3 chan_only(const DevScene &S, uint32_t ch, const V3 &a) {
     return V3{ch == 0 ? a.x : 0.0f * a.x, ch == 1 ? a.y : 0.0f * a.y, ch == 2 ? a.z : 0.0f * a.z};
 }
 
-#ifndef NORI_SHADE_ATOMIC_REC
-#define NORI_SHADE_ATOMIC_REC 1
-#endif
 // Emission found by the shade kernel, added to the sample record.  Each record
 // has one path, and the shadow kernel's read-modify-write of it runs in a later
 // launch, so the adds need no atomicity -- but returnless atomics do not make
@@ -1437,15 +1255,10 @@ ND void rec_add(const DevScene &S, float4 *rec, PathState &ps, const V3 &a0) {
         ps.L = ps.L + a;
         return;
     }
-#if NORI_SHADE_ATOMIC_REC
     float *r = reinterpret_cast<float *>(rec + ps.work);
     atomicAdd(r + 0, a.x);
     atomicAdd(r + 1, a.y);
     atomicAdd(r + 2, a.z);
-#else
-    const float4 L = rec[ps.work];
-    rec[ps.work] = make_float4(L.x + a.x, L.y + a.y, L.z + a.z, L.w);
-#endif
 }
 
 // Deviation D10: a mirror or dielectric BSDF evaluates to exactly zero, so
@@ -1589,11 +1402,6 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         }
         rec_add<ATOMIC>(S, rec, ps, Ladd);
     }
-#ifdef NORI_PROF_NO_NEE  // profiling build only: NEE replaced by its three random draws
-    if (MIS) {
-        pcg_skip(ps.rng, 3);
-    } else
-#endif
     if (MIS && skip_nee(S, B, ps.beta)) {
         pcg_skip3(ps.rng);  // deviation D10: the three NEE draws, unused
     } else if (MIS) {  // next-event estimation (path_mis.cpp:42-61)
@@ -1623,14 +1431,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
     br.uv = hs.uv;
     br.wo = V3{0, 0, 1};
     br.measure = kMeasureUnknown;
-#ifdef NORI_PROF_NO_SAMPLE  // profiling build only: a cheap reflection instead of BSDF sampling
-    V2 su = next2D(ps.rng);
-    br.wo = V3{su.x - 0.5f, su.y - 0.5f, 0.5f};
-    br.measure = kMeasureSolidAngle;
-    V3 w = V3{0.7f, 0.7f, 0.7f};
-#else
     V3 w = bsdf_sample<FULL>(B, br, next2D(ps.rng));
-#endif
     if (is_zero(w)) return false;  // deviation D1: zero-weight samples end the path
     ps.beta = ps.beta * w;
     if (MIS) {
@@ -1712,16 +1513,6 @@ ND void next_channel(const DevScene &S, const WorkDesc &wd, PathState &ps) {
     ps.prev = -1.0f;
 }
 
-// Closest hit of a path's ray (scan mode, TRACE builds of k_shade).
-ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
-    TRay r{ps.o, ps.d, V3{0, 0, 0}, ps.mint, ps.maxt};
-    float t, u, v;
-    uint32_t p;
-    uint32_t *no_stack = nullptr;
-    traverse<0, false>(S, r, no_stack, t, p, u, v);
-    *hit = make_float4(t, __uint_as_float(p), u, v);
-}
-
 #ifndef NORI_SHADE_WAVES
 #define NORI_SHADE_WAVES 5
 #endif
@@ -1731,14 +1522,11 @@ ND void trace_into(const DevScene &S, const PathState &ps, float4 *hit) {
 // lds_bytes != 0: the scene blob is staged into LDS first, so the chains of
 // dependent table reads of a vertex (shape -> bsdf -> vertices -> light CDF)
 // run at LDS instead of L2 latency.
-// TRACE (scan-mode scenes): the closest hit of every outgoing ray is found
-// here as well (wave-uniform scan, traverse<0>), so the rays do not make a
-// round trip through HBM to a separate extension kernel.
 // LDS is a template parameter, not a run-time choice: with the scene pointers
 // known to point into LDS the compiler emits ds_read for the table reads; a
 // run-time select between the LDS and the global tables leaves generic
 // pointers, i.e. flat loads (vector-memory latency, both wait counters).
-template <int INTEG, bool TRACE, bool LDS, int VAR>
+template <int INTEG, bool LDS, int VAR>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(NORI_SHADE_WAVES)))
 void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState seg, int in_sel, WorkDesc wd,
              float4 *rec, Counters *C, uint32_t lds_bytes) {
@@ -1850,7 +1638,6 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         sq.ray_d[i] = make_float4(so.d.x, so.d.y, so.d.z, so.maxt);
         sq.payload[i] = make_float4(so.contrib.x, so.contrib.y, so.contrib.z, __uint_as_float(so.work));
     }
-    if (TRACE && alive) trace_into(Sg, ps, out.hit + b * kSeg + al_off);
     if (alive) store_path(out, b * kSeg + al_off, ps);
     NORI_SPHASE(3)
     // ---- regeneration: the free slots [al_tot, kSeg) take the next work ids of
@@ -1861,7 +1648,6 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         if (wn != ~0u) {
             PathState np;
             regen_path<FULL>(Sg, wd, wn, s_pix[tid - al_tot], np, rec);
-            if (TRACE) trace_into(Sg, np, out.hit + q);
             store_path(out, q, np);
         }
     }
@@ -2792,39 +2578,35 @@ hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int a
 #if NORI_TU == 1
 template <int INTEG, int VAR>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                           const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
+                           const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
     dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
-    if (trace && lds)
-        hipLaunchKernelGGL((k_shade<INTEG, true, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
-    else if (trace)
-        hipLaunchKernelGGL((k_shade<INTEG, true, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
-    else if (lds)
-        hipLaunchKernelGGL((k_shade<INTEG, false, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+    if (lds)
+        hipLaunchKernelGGL((k_shade<INTEG, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
-        hipLaunchKernelGGL((k_shade<INTEG, false, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+        hipLaunchKernelGGL((k_shade<INTEG, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
 }
 template <int INTEG>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                           const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
+                           const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
-    if (S.basic) shade_dispatch<INTEG, 0>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
-    else if (S.chroma) shade_dispatch<INTEG, 2>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
-    else shade_dispatch<INTEG, 1>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+    if (S.basic) shade_dispatch<INTEG, 0>(S, in, out, sq, seg, in_sel, wd, rec, C, lds, nseg, st);
+    else if (S.chroma) shade_dispatch<INTEG, 2>(S, in, out, sq, seg, in_sel, wd, rec, C, lds, nseg, st);
+    else shade_dispatch<INTEG, 1>(S, in, out, sq, seg, in_sel, wd, rec, C, lds, nseg, st);
 }
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
-                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C, bool trace,
+                        const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                         uint32_t nseg, hipStream_t st) {
     if (nseg == 0 || wd.b0 + nseg > wd.G) return hipErrorInvalidValue;
     const uint32_t lds = S.blob_bytes <= kShadeLdsMax ? S.blob_bytes : 0u;
     switch (S.integrator) {
     case NORI_INTEGRATOR_PATH_MATS:
-        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+        shade_dispatch<NORI_INTEGRATOR_PATH_MATS>(S, in, out, sq, seg, in_sel, wd, rec, C, lds, nseg, st);
         break;
     case NORI_INTEGRATOR_VOLUMETRIC:
-        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st);
+        shade_dispatch<NORI_INTEGRATOR_VOLUMETRIC>(S, in, out, sq, seg, in_sel, wd, rec, C, lds, nseg, st);
         break;
-    default: shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, trace, lds, nseg, st); break;
+    default: shade_dispatch<NORI_INTEGRATOR_PATH_MIS>(S, in, out, sq, seg, in_sel, wd, rec, C, lds, nseg, st); break;
     }
     return hipGetLastError();
 }
@@ -2865,69 +2647,6 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     }
     return hipGetLastError();
-}
-
-hipError_t launch_extend_sorted(const DevScene &S, const PathQueue &q, const uint32_t *order, const uint32_t *n,
-                                uint32_t slots, int stack, hipStream_t st) {
-    const dim3 g((slots + kTraceBlock - 1) / kTraceBlock), b(kTraceBlock);
-    switch (stack) {
-    case 8: hipLaunchKernelGGL(k_extend_sorted<8>, g, b, 0, st, S, q, order, n); break;
-    case 16: hipLaunchKernelGGL(k_extend_sorted<16>, g, b, 0, st, S, q, order, n); break;
-    case 32: hipLaunchKernelGGL(k_extend_sorted<32>, g, b, 0, st, S, q, order, n); break;
-    case 64: hipLaunchKernelGGL(k_extend_sorted<64>, g, b, 0, st, S, q, order, n); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-hipError_t launch_shadow_sorted(const DevScene &S, const ShadowQueue &sq, const uint32_t *order, const uint32_t *n,
-                                float4 *rec, uint32_t slots, int stack, hipStream_t st) {
-    const dim3 g((slots + kTraceBlock - 1) / kTraceBlock), b(kTraceBlock);
-    switch (stack) {
-    case 8: hipLaunchKernelGGL(k_shadow_sorted<8>, g, b, 0, st, S, sq, order, n, rec); break;
-    case 16: hipLaunchKernelGGL(k_shadow_sorted<16>, g, b, 0, st, S, sq, order, n, rec); break;
-    case 32: hipLaunchKernelGGL(k_shadow_sorted<32>, g, b, 0, st, S, sq, order, n, rec); break;
-    case 64: hipLaunchKernelGGL(k_shadow_sorted<64>, g, b, 0, st, S, sq, order, n, rec); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <bool ANY>
-static hipError_t pt_dispatch(const DevScene &S, const PtJob<ANY> &J, const uint32_t *cnt, uint32_t G, int stack,
-                              uint32_t *ctr, uint32_t blocks, hipStream_t st) {
-    const dim3 g(blocks), b(kTraceBlock);
-    switch (stack) {
-    case 8: hipLaunchKernelGGL((k_trace_pt<8, ANY>), g, b, 0, st, S, J, cnt, G, ctr); break;
-    case 16: hipLaunchKernelGGL((k_trace_pt<16, ANY>), g, b, 0, st, S, J, cnt, G, ctr); break;
-    case 32: hipLaunchKernelGGL((k_trace_pt<32, ANY>), g, b, 0, st, S, J, cnt, G, ctr); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-hipError_t launch_extend_pt(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
-                            uint32_t *ctr, uint32_t blocks, hipStream_t st) {
-    PtJob<false> J{q.ray_o, q.ray_d, q.hit, nullptr, nullptr};
-    return pt_dispatch<false>(S, J, cnt, G, stack, ctr, blocks, st);
-}
-hipError_t launch_shadow_pt(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
-                            int stack, uint32_t *ctr, uint32_t blocks, hipStream_t st) {
-    PtJob<true> J{sq.ray_o, sq.ray_d, nullptr, sq.payload, rec};
-    return pt_dispatch<true>(S, J, shcnt, G, stack, ctr, blocks, st);
-}
-// Resident work-groups per CU of the persistent traversal kernel.
-int pt_blocks_per_cu(int stack, bool any) {
-    int n = 0;
-    hipError_t e = hipErrorInvalidValue;
-    switch (stack) {
-    case 8: e = any ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<8, true>, kTraceBlock, 0)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<8, false>, kTraceBlock, 0); break;
-    case 16: e = any ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<16, true>, kTraceBlock, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<16, false>, kTraceBlock, 0); break;
-    case 32: e = any ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<32, true>, kTraceBlock, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_pt<32, false>, kTraceBlock, 0); break;
-    default: break;
-    }
-    return e == hipSuccess ? n : 0;
 }
 
 // Start of a chunk of passes: zero the counters, the segments' path counts,

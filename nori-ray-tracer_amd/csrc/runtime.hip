@@ -193,7 +193,7 @@ struct nori_gpu_ctx {
     hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
     nori_camera_desc cam{};
-    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob;
+    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, scan_boxes;
     DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
     uint32_t spp = 1;    // the scene's sampleCount (default pass count)
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
@@ -203,12 +203,8 @@ struct nori_gpu_ctx {
     std::atomic<float> progress{1.0f};
     // render state
     DevBuf q[2][5], sq[3], seg[4], segstats, tailpre, rec, counters, pixels, blocks, film;
-    DevBuf ptctr;                    // persistent traversal work counters, 4 per part
-    DevBuf rsort[5];                 // ray reordering (raysort.hip): keys x2, slots x2 (pool each), sort scratch per part
-    DevBuf rsort_n;                  // ... and the ray count of each part's sorted launch
     DevBuf varbuf;                   // per-pixel sample statistics when variance_out is a host buffer
     DevBuf ph, ph_rgbe, ph_tab, ph_start;             // photonmapper: photon map (photon_map.cpp) and its hash-grid buckets
-    uint32_t pt_grid[2] = {0, 0};    // persistent grid of extend / shadow (0 = per-ray launches)
     uint32_t pool_cap = 0;
     uint32_t *pinned = nullptr;      // host-mapped flags: [0] done, [1] exhausted segments
     uint32_t *pinned_dev = nullptr;  // device view of `pinned`
@@ -373,6 +369,61 @@ void mark_solitary_spheres(const nori_scene_desc &d, const float rmin[3], const 
         }
         shapes[s].solitary = ok ? 1 : 0;
         if (std::getenv("NORI_DEBUG")) std::fprintf(stderr, "[nori] sphere shape %u: solitary %d\n", s, (int)ok);
+    }
+}
+
+// Filter groups of the scan-mode trace kernels (kernels.hip scan_filtered):
+// the scan's triangles are paired greedily (each with the unpaired triangle
+// whose leaf box joins its own into the smallest surface area -- the two
+// halves of a wall quad), and a group carries the union of its members'
+// reference leaf boxes and the bit mask of their scan indices, as
+// (min.xyz, mask bits 0-31) (max.xyz, mask bits 32-63).  None when the scan
+// holds more than 64 triangles (a forced scan of a larger scene) or with
+// NORI_SCAN_FILTER=0 (A/B): the kernels then test every primitive.
+template <class IsSphere>
+void build_scan_groups(const DeviceBvh &bvh, uint32_t n, IsSphere is_sphere, uint32_t scan_tris,
+                       std::vector<float> &out) {
+    out.clear();
+    if (const char *e = std::getenv("NORI_SCAN_FILTER"); e && e[0] == '0') return;
+    if (scan_tris > 64) return;
+    struct Item {
+        uint32_t scan;  // index in the scan list
+        float mn[3], mx[3];
+    };
+    std::vector<Item> tris;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (is_sphere(i)) continue;
+        Item it;
+        it.scan = (uint32_t)tris.size();
+        for (int k = 0; k < 3; ++k) it.mn[k] = bvh.leaf_box[6 * (size_t)i + k], it.mx[k] = bvh.leaf_box[6 * (size_t)i + 3 + k];
+        tris.push_back(it);
+    }
+    auto join_area = [](const Item &a, const Item &b) {
+        float d[3];
+        for (int k = 0; k < 3; ++k) d[k] = std::max(a.mx[k], b.mx[k]) - std::min(a.mn[k], b.mn[k]);
+        return (double)d[0] * d[1] + (double)d[1] * d[2] + (double)d[2] * d[0];
+    };
+    std::vector<char> used(tris.size(), 0);
+    for (size_t a = 0; a < tris.size(); ++a) {
+        if (used[a]) continue;
+        used[a] = 1;
+        int best = -1;
+        double ba = 0;
+        for (size_t b = a + 1; b < tris.size(); ++b)
+            if (!used[b] && (best < 0 || join_area(tris[a], tris[b]) < ba)) best = (int)b, ba = join_area(tris[a], tris[b]);
+        Item g = tris[a];
+        uint64_t mask = 1ull << tris[a].scan;
+        if (best >= 0) {
+            used[(size_t)best] = 1;
+            const Item &o = tris[(size_t)best];
+            for (int k = 0; k < 3; ++k) g.mn[k] = std::min(g.mn[k], o.mn[k]), g.mx[k] = std::max(g.mx[k], o.mx[k]);
+            mask |= 1ull << o.scan;
+        }
+        const uint32_t lo = (uint32_t)mask, hi = (uint32_t)(mask >> 32);
+        float w[2];
+        std::memcpy(&w[0], &lo, 4);
+        std::memcpy(&w[1], &hi, 4);
+        out.insert(out.end(), {g.mn[0], g.mn[1], g.mn[2], w[0], g.mx[0], g.mx[1], g.mx[2], w[1]});
     }
 }
 
@@ -606,6 +657,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     // scan order: triangles (leaf order) padded to kScanGroup with records no
     // ray hits (zero edges: det = 0, or NaN t), then spheres (leaf order)
     std::vector<float> scan_prims;
+    std::vector<float> scan_boxes;  // filter groups of the scan kernels: (min, mask lo) (max, mask hi)
     uint32_t scan_tris = 0;
     if (scan) {
         auto is_sphere = [&](uint32_t i) {
@@ -627,6 +679,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         }
         for (uint32_t i = 0; i < off; ++i)
             if (is_sphere(i)) add(i);
+        build_scan_groups(bvh, off, is_sphere, scan_tris, scan_boxes);
     }
     const std::vector<float> &prim_list = scan ? scan_prims : bvh.prims;
 
@@ -644,6 +697,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     if (cdf.empty()) cdf.assign(1, 0.0f);
     c.nodes.upload(bvh.nodes);
     c.prims.upload(prim_list);
+    if (!scan_boxes.empty()) c.scan_boxes.upload(scan_boxes);
     c.tri_vidx.upload(tri_vidx);
     c.pos.upload(pos);
     c.nrm.upload(nrm);
@@ -694,6 +748,8 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.num_nodes = bvh.num_nodes;
     S.num_prims = (uint32_t)(prim_list.size() / 12);
     S.num_scan_tris = scan_tris;
+    S.scan_boxes = scan_boxes.empty() ? nullptr : c.scan_boxes.as<float4>();
+    S.num_scan_boxes = (uint32_t)(scan_boxes.size() / 8);
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     S.blob = use_blob ? c.blob.as<float4>() : nullptr;
     S.blob_bytes = use_blob ? (uint32_t)blob.size() : 0u;
@@ -822,29 +878,6 @@ uint32_t pool_parts(bool bvh) {
     const long v = e ? std::atol(e) : (long)def;
     return (uint32_t)(v >= 1 && v <= kMaxParts ? v : def);
 }
-uint64_t event_every() {  // NORI_EVENT_EVERY: iterations per host event (default 1)
-    const char *e = std::getenv("NORI_EVENT_EVERY");
-    const long v = e ? std::atol(e) : 1;
-    return v >= 1 && v <= 8 ? (uint64_t)v : 1;
-}
-// NORI_LOOKAHEAD / NORI_LOOKAHEAD_END: iterations queued ahead of the
-// termination check, before / after the first work stream ran dry
-uint64_t lookahead(const char *name, int dflt) {
-    const char *e = std::getenv(name);
-    const long v = e ? std::atol(e) : dflt;
-    return v >= 1 && v <= kRing - 2 ? (uint64_t)v : (uint64_t)dflt;
-}
-// NORI_RAY_SORT: bits per axis of the origin Morton code that orders the BVH
-// walks of each launch (raysort.hip); 0 = queue order.
-int ray_sort_bits() {
-    const char *e = std::getenv("NORI_RAY_SORT");
-    const long v = e ? std::atol(e) : 0;
-    return v >= 0 && v <= 9 ? (int)v : 0;
-}
-bool fused_extend() {
-    const char *e = std::getenv("NORI_FUSED_EXTEND");
-    return e && e[0] == '1';
-}
 // Sample passes folded by one splat work-group.  Default: about one
 // work-group per CU over the whole launch (passes x blocks / 256), so the
 // splat leaves most of the chip to the tail finisher it overlaps with
@@ -858,33 +891,6 @@ uint32_t splat_passes(uint32_t np, size_t nblocks, uint32_t target_wgs = 256) {
     if (v < 1) v = 1;
     return (uint32_t)std::min<long>(v, np);
 }
-bool overlap_splat() {
-    const char *e = std::getenv("NORI_SPLAT_OVERLAP");
-    return !(e && e[0] == '0');
-}
-// NORI_PT=1: persistent traversal of the BVH scenes (k_trace_pt) with a grid
-// of the device's resident work-groups times NORI_PT_OCC (default 1).  Off by
-// default: interleaved A/B on MI355X (C3 height field, table scene) measured
-// -13..+3 % on C3 and -10..+7 % on the table against the one-ray-per-thread
-// launches, i.e. no reliable gain.
-void setup_persistent(nori_gpu_ctx &c) {
-    c.pt_grid[0] = c.pt_grid[1] = 0;
-    const char *e = std::getenv("NORI_PT");
-    if (c.stack == 0 || !(e && e[0] == '1')) return;
-    if (c.stack != 8 && c.stack != 16 && c.stack != 32) return;
-    int cus = 0;
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
-    const char *o = std::getenv("NORI_PT_OCC");
-    double occ = o ? std::atof(o) : 1.0;
-    if (!(occ > 0.0 && occ <= 1.0)) occ = 1.0;
-    for (int k = 0; k < 2; ++k) {
-        const int per_cu = pt_blocks_per_cu(c.stack, k == 1);
-        c.pt_grid[k] = (uint32_t)std::max(1.0, occ * per_cu * cus);
-    }
-    c.ptctr.ensure(4 * 4 * kMaxParts);
-    HIP_TRY(hipMemset(c.ptctr.p, 0, 4 * 4 * kMaxParts));
-}
-
 // Per-pixel sample statistics (render_desc.variance_out): the device buffer
 // the kernels add into -- the caller's own when it is device memory, else a
 // zeroed scratch buffer that var_finish adds into the host array.
@@ -1187,15 +1193,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     };
     auto timed = [&](int kind, auto &&launch) { timed_on(c.stream, kind, launch); };
     bool cancelled = false;
-    // NORI_FUSED_EXTEND=1: scan-mode scenes trace the extension rays inside
-    // the shade kernel (measured even with separate k_extend launches)
-    const bool fused = c.stack == 0 && fused_extend();
-    const int rsort_bits = c.stack != 0 && !c.pt_grid[0] ? ray_sort_bits() : 0;
-    const uint64_t every = event_every(), ahead = lookahead("NORI_LOOKAHEAD", kLookahead),
-                   ahead_end = lookahead("NORI_LOOKAHEAD_END", kLookaheadEnd);
     const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(pool_parts(c.stack != 0), pool / kSeg));
-    const char *stg = std::getenv("NORI_PART_STAGGER");
-    const bool stagger = stg && stg[0] == '1';
     const uint32_t G = pool / kSeg;
     SegState seg{{c.seg[0].as<uint32_t>(), c.seg[1].as<uint32_t>()}, c.seg[2].as<uint32_t>(), c.seg[3].as<uint32_t>(),
                  c.segstats.as<uint4>()};
@@ -1230,23 +1228,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         std::vector<ShadowQueue> sqh(parts);
         std::vector<SegState> segh(parts);
         std::vector<WorkDesc> wdh(parts);
-        // ray reordering of the BVH walks: per part, a window of the key /
-        // slot buffers (slot indices are part-local) and its own scratch
-        std::vector<RaySortBufs> rsb(parts);
-        if (rsort_bits) {
-            uint32_t gmax = 0;
-            for (uint32_t h = 0; h < parts; ++h) gmax = std::max(gmax, Gp[h]);
-            const size_t tb = (ray_sort_temp_bytes(gmax * kSeg, rsort_bits) + 255) / 256 * 256;
-            for (int k = 0; k < 4; ++k) c.rsort[k].ensure(4 * (size_t)pool);
-            c.rsort[4].ensure(tb * parts);
-            c.rsort_n.ensure(4 * kMaxParts);
-            for (uint32_t h = 0; h < parts; ++h) {
-                const size_t e = (size_t)base[h] * kSeg;
-                rsb[h] = RaySortBufs{{c.rsort[0].as<uint32_t>() + e, c.rsort[1].as<uint32_t>() + e},
-                                     {c.rsort[2].as<uint32_t>() + e, c.rsort[3].as<uint32_t>() + e},
-                                     c.rsort[4].as<char>() + tb * h, tb, c.rsort_n.as<uint32_t>() + h};
-            }
-        }
         for (uint32_t h = 0; h < parts; ++h) {
             Qh[h][0] = q_view(Q[0], base[h]);
             Qh[h][1] = q_view(Q[1], base[h]);
@@ -1259,8 +1240,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         HIP_TRY(hipEventRecord(c.fork, c.stream));  // the part streams start after the resets above
         for (uint32_t h = 1; h < parts; ++h) HIP_TRY(hipStreamWaitEvent(c.parts[h], c.fork, 0));
-        uint64_t lag = (ahead + every - 1) / every;
-        const uint64_t lag_end = (ahead_end + every - 1) / every;
+        uint64_t lag = kLookahead;
         for (uint64_t it = 0;; ++it) {
             int in = (int)(it & 1), out = in ^ 1;
             last_out = out;
@@ -1269,50 +1249,17 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                 const SegState &sg = segh[h];
                 timed_on(st, 2, [&] {
                     return launch_shade(S, Qh[h][in], Qh[h][out], sqh[h], sg, in, wdh[h], c.rec.as<float4>(), C,
-                                        fused, Gp[h], st);
+                                        Gp[h], st);
                 });
-                if (it == 0 && h == 0 && parts > 1 && stagger) {
-                    // NORI_PART_STAGGER=1: the other parts start after part 0's first shade
-                    HIP_TRY(hipEventRecord(c.fork, c.stream));
-                    for (uint32_t k = 1; k < parts; ++k) HIP_TRY(hipStreamWaitEvent(c.parts[k], c.fork, 0));
-                }
-                uint32_t *ctr = c.pt_grid[0] ? c.ptctr.as<uint32_t>() + 4 * h : nullptr;
-                if (rsort_bits) {
-                    const RaySortBufs &R = rsb[h];
-                    const uint32_t slots = Gp[h] * kSeg;
-                    // the sorts' time is counted with the walks they order
-                    timed_on(st, 0, [&] {
-                        return launch_ray_sort(S, Qh[h][out].ray_o, Qh[h][out].ray_d, sg.cnt[out], Gp[h], rsort_bits,
-                                               R, st);
-                    });
-                    timed_on(st, 0, [&] {
-                        return launch_extend_sorted(S, Qh[h][out], R.vals[1], R.n, slots, c.stack, st);
-                    });
-                    timed_on(st, 1, [&] {
-                        return launch_ray_sort(S, sqh[h].ray_o, sqh[h].ray_d, sg.shcnt, Gp[h], rsort_bits, R, st);
-                    });
-                    timed_on(st, 1, [&] {
-                        return launch_shadow_sorted(S, sqh[h], R.vals[1], R.n, c.rec.as<float4>(), slots, c.stack, st);
-                    });
-                    continue;
-                }
-                if (!fused)
-                    timed_on(st, 0, [&] {
-                        return ctr ? launch_extend_pt(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, ctr, c.pt_grid[0], st)
-                                   : launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st);
-                    });
+                timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st); });
                 timed_on(st, 1, [&] {
-                    return ctr ? launch_shadow_pt(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, ctr + 2,
-                                                  c.pt_grid[1], st)
-                               : launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st);
+                    return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st);
                 });
             }
             ++iters;
-            // an event every `every` iterations (each record adds a gap
-            // between dependent kernels); the host waits on the one from at
-            // least kLookahead iterations back
-            if ((it + 1) % every != 0) continue;
-            const uint64_t ev = it / every;
+            // an event per iteration; the host waits on the one from `lag`
+            // iterations back
+            const uint64_t ev = it;
             for (uint32_t h = 0; h < parts; ++h)
                 HIP_TRY(hipEventRecord(c.ring[h][ev % kRing], h ? c.parts[h] : c.stream));
             if (ev >= lag) {
@@ -1321,7 +1268,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                 // the streams are running dry: queue fewer iterations ahead,
                 // so that few drain iterations (full-grid launches over a
                 // thinning pool) are already queued when the last one does
-                if (exhausted) lag = std::min(lag, lag_end);
+                if (exhausted) lag = std::min<uint64_t>(lag, kLookaheadEnd);
                 c.progress = (float)std::min(1.0, (double)done_before / (double)total_all +
                                                       (double)np / passes * exhausted / G);
                 // every work id has been handed out: finish the remaining paths in one launch
@@ -1340,9 +1287,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         // The samples still in flight are marked pending; the film splat of all
         // the others runs on the side stream while the finisher completes the
         // pending ones and splats each itself.
-        // (NORI_SPLAT_OVERLAP=0: splat after the finisher on the same stream.)
-        const bool overlap = overlap_splat();
-        hipStream_t splat_st = overlap ? c.side : c.stream;
+        hipStream_t splat_st = c.side;
         HIP_TRY(launch_mark(Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stream));
         HIP_TRY(hipEventRecord(c.fork, c.stream));
         HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));
@@ -1497,12 +1442,42 @@ nori_gpu_render_desc shard_of(int W, int H, uint32_t spp, const nori_gpu_render_
     return out;
 }
 
-// Watchdog of the film exchange (NORI_COMM_TIMEOUT_S, default 600 s): how long
-// a rank waits for its peers in a collective before aborting the communicator.
-double comm_timeout_s() {
-    const char *e = std::getenv("NORI_COMM_TIMEOUT_S");
-    const double v = e ? std::atof(e) : 0.0;
-    return v > 0.0 ? v : 600.0;
+// Samples of a share (pass count x pixels of its blocks, or of the image).
+double share_samples(int W, int H, const nori_gpu_render_desc &s) {
+    if (!s.num_blocks) return (double)s.pass_count * W * H;
+    const int nx = (W + NORI_BLOCK_SIZE - 1) / NORI_BLOCK_SIZE;
+    double px = 0;
+    for (uint32_t i = 0; i < s.num_blocks; ++i) {
+        const int bx = (int)(s.block_ids[i] % (uint32_t)nx), by = (int)(s.block_ids[i] / (uint32_t)nx);
+        px += (double)std::min(NORI_BLOCK_SIZE, W - bx * NORI_BLOCK_SIZE) * std::min(NORI_BLOCK_SIZE, H - by * NORI_BLOCK_SIZE);
+    }
+    return px * s.pass_count;
+}
+
+// Watchdog of the collectives of a sharded render: how long a rank waits in
+// the status exchange or the film sum for its peers before it aborts the
+// communicator.  Only a peer that cannot join at all (its device faulted,
+// its process died) is waited for: every other failure reaches the peers
+// through the status exchange.  NORI_COMM_TIMEOUT_S fixes the bound;
+// otherwise it scales with the frame: max(30 s, 20 x this rank's own render
+// time x largest share / own share), since every peer renders a share of
+// about the same size with the same code.  A rank without a share has no time
+// of its own and waits up to 600 s.
+double comm_timeout_s(double own_s, double own_samples, double max_samples) {
+    if (const char *e = std::getenv("NORI_COMM_TIMEOUT_S")) {
+        const double v = std::atof(e);
+        if (v > 0.0) return v;
+    }
+    if (!(own_samples > 0.0)) return 600.0;
+    return std::max(30.0, 20.0 * own_s * std::max(1.0, max_samples / own_samples));
+}
+
+// Status word of the exchange: severity << 16 | rank, reduced by max over the
+// ranks, so the worst outcome wins and names its rank (the highest of equals).
+// Severity 0 rendered, 1 cancelled, 2 failed.
+int comm_status_word(int rc, int rank) {
+    const int sev = rc == NORI_OK ? 0 : (rc == NORI_ERR_CANCELLED ? 1 : 2);
+    return (sev << 16) | (rank & 0xFFFF);
 }
 
 }  // namespace
@@ -1644,7 +1619,6 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
         upload_scene(*c, *d);
-        setup_persistent(*c);
         if (d->integrator == NORI_INTEGRATOR_PHOTONMAPPER) photon_preprocess(*c, *d);
         *out = c.release();
         return NORI_OK;
@@ -1692,7 +1666,13 @@ int nori_gpu_comm_id(unsigned char *id) {
 int nori_gpu_comm_create(const unsigned char *id, int nranks, int rank, int device, nori_gpu_comm **out) {
     return guarded([&] {
         if (!id || !out) return fail(NORI_ERR_INVALID, "null argument");
+        if (nranks < 1 || nranks > 0xFFFF || rank < 0 || rank >= nranks) return fail(NORI_ERR_INVALID, "rank out of range");
         std::unique_ptr<nori_gpu_comm> c(new nori_gpu_comm);
+        // the status exchange's words, allocated here so that no allocation
+        // stands between a failed share and the exchange
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipMalloc((void **)&c->status_dev, sizeof(int)));
+        HIP_TRY(hipHostMalloc((void **)&c->status_host, sizeof(int), hipHostMallocDefault));
         c->nccl = comm_create(id, nranks, rank, device);
         c->nranks = nranks;
         c->rank = rank;
@@ -1732,55 +1712,68 @@ int nori_gpu_shard_desc(const nori_scene_desc *d, const nori_gpu_render_desc *rd
 int nori_gpu_render_sharded(nori_gpu_ctx *c, nori_gpu_comm *comm, const nori_gpu_render_desc *rd, int mode, int root,
                             float *film, nori_gpu_stats *stats) {
     return guarded([&] {
-        if (!c || !comm || !rd || !film) return fail(NORI_ERR_INVALID, "null argument");
-        if (rd->num_blocks && !rd->block_ids) return fail(NORI_ERR_INVALID, "block_ids is null");
-        if (rd->variance_out)  // per-pixel statistics are not summed across ranks
-            return fail(NORI_ERR_INVALID, "nori_gpu_render_sharded: variance_out must be NULL");
-        if (root >= comm->nranks) return fail(NORI_ERR_INVALID, "root out of range");
-        if (comm->device != c->device) return fail(NORI_ERR_INVALID, "communicator and context on different devices");
+        if (!c || !comm) return fail(NORI_ERR_INVALID, "null argument");
         if (comm->aborted) return fail(NORI_ERR_HIP, "communicator was aborted by an earlier failure");
-        HIP_TRY(hipSetDevice(c->device));
-        std::vector<uint32_t> blocks;
-        nori_gpu_render_desc s = shard_of(c->S.W, c->S.H, c->spp, *rd, mode, comm->nranks, comm->rank, blocks);
-        s.output_on_device = 1;
-        s.variance_out = nullptr;
-        const size_t n = 4 * (size_t)(c->S.W + 2 * c->S.border) * (size_t)(c->S.H + 2 * c->S.border);
-        HIP_TRY(hipMemsetAsync(film, 0, n * sizeof(float), c->stream));
         // This rank's share.  A failure or a cancel (nori_gpu_cancel) must not
         // leave the peers blocked in the film sum: every rank joins a status
         // exchange first (max over ranks of severity << 16 | rank), and the
-        // film sum runs only if every rank rendered its share.
+        // film sum runs only if every rank rendered its share.  Everything
+        // fallible of the share -- argument checks, the film clear, the
+        // render -- reports through the exchange.
         int rc = NORI_OK;
         std::string err;
-        if (s.pass_count) {
-            try {
-                rc = render(*c, s, film, stats);
-            } catch (const NoriException &e) {
-                rc = e.code;
-                err = e.what();
-            } catch (const std::bad_alloc &) {
-                rc = NORI_ERR_OOM;
-                err = "out of memory";
-            }
-            if (rc != NORI_OK && err.empty()) err = g_last_error;
-        } else if (stats) {
-            std::memset(stats, 0, sizeof(*stats));
+        double own_s = 0.0, own_samples = 0.0, max_samples = 0.0;
+        size_t n = 0;
+        try {
+            if (!rd || !film) throw NoriException(NORI_ERR_INVALID, "null argument");
+            if (rd->num_blocks && !rd->block_ids) throw NoriException(NORI_ERR_INVALID, "block_ids is null");
+            if (rd->variance_out)  // per-pixel statistics are not summed across ranks
+                throw NoriException(NORI_ERR_INVALID, "nori_gpu_render_sharded: variance_out must be NULL");
+            if (root >= comm->nranks) throw NoriException(NORI_ERR_INVALID, "root out of range");
+            if (comm->device != c->device)
+                throw NoriException(NORI_ERR_INVALID, "communicator and context on different devices");
+            HIP_TRY(hipSetDevice(c->device));
+            std::vector<uint32_t> blocks, other;
+            nori_gpu_render_desc s = shard_of(c->S.W, c->S.H, c->spp, *rd, mode, comm->nranks, comm->rank, blocks);
+            own_samples = share_samples(c->S.W, c->S.H, s);
+            for (int r = 0; r < comm->nranks; ++r)
+                max_samples = std::max(max_samples, share_samples(c->S.W, c->S.H,
+                                                                  shard_of(c->S.W, c->S.H, c->spp, *rd, mode,
+                                                                           comm->nranks, r, other)));
+            s.output_on_device = 1;
+            s.variance_out = nullptr;
+            n = 4 * (size_t)(c->S.W + 2 * c->S.border) * (size_t)(c->S.H + 2 * c->S.border);
+            HIP_TRY(hipMemsetAsync(film, 0, n * sizeof(float), c->stream));
+            const auto t0 = std::chrono::steady_clock::now();
+            if (s.pass_count) rc = render(*c, s, film, stats);
+            else if (stats) std::memset(stats, 0, sizeof(*stats));
+            own_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        } catch (const NoriException &e) {
+            rc = e.code;
+            err = e.what();
+        } catch (const std::bad_alloc &) {
+            rc = NORI_ERR_OOM;
+            err = "out of memory";
+        } catch (const std::exception &e) {
+            rc = NORI_ERR_INVALID;
+            err = e.what();
         }
-        const double timeout = comm_timeout_s();
+        if (rc != NORI_OK && err.empty()) err = g_last_error;
         if (rc == NORI_ERR_HIP) {
-            // the device or its stream may be unusable: abort, so the peers'
-            // status exchange fails (they see the abort or time out) instead of hanging
-            comm_abort(comm->nccl);
-            comm->aborted = true;
-            return fail(rc, err);
+            // A sticky error (a device fault) fails every later call on the
+            // device, so this rank cannot join the exchange: abort, and the
+            // peers' watchdog ends their wait.  Any other HIP error leaves
+            // the stream usable and goes through the exchange.
+            (void)hipGetLastError();
+            if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+                comm_abort(comm->nccl);
+                comm->aborted = true;
+                return fail(rc, err);
+            }
         }
-        if (!comm->status_dev) {
-            HIP_TRY(hipMalloc((void **)&comm->status_dev, sizeof(int)));
-            HIP_TRY(hipHostMalloc((void **)&comm->status_host, sizeof(int), hipHostMallocDefault));
-        }
-        const int sev = rc == NORI_OK ? 0 : (rc == NORI_ERR_CANCELLED ? 1 : 2);
-        const int all = comm_max_int(comm->nccl, comm->status_dev, comm->status_host, (sev << 16) | comm->rank,
-                                     c->stream, timeout, comm->aborted);
+        const double timeout = comm_timeout_s(own_s, own_samples, max_samples);
+        const int all = comm_max_int(comm->nccl, comm->status_dev, comm->status_host,
+                                     comm_status_word(rc, comm->rank), c->stream, timeout, comm->aborted);
         if (rc != NORI_OK) return fail(rc, err);
         if ((all >> 16) != 0)
             return fail((all >> 16) == 1 ? NORI_ERR_CANCELLED : NORI_ERR_INVALID,
@@ -1790,6 +1783,10 @@ int nori_gpu_render_sharded(nori_gpu_ctx *c, nori_gpu_comm *comm, const nori_gpu
         comm_wait(comm->nccl, c->stream, timeout, comm->aborted);
         return (int)NORI_OK;
     });
+}
+int nori_gpu_comm_status_word(int rc, int rank) { return comm_status_word(rc, rank); }
+double nori_gpu_comm_timeout(double own_seconds, double own_samples, double max_samples) {
+    return comm_timeout_s(own_seconds, own_samples, max_samples);
 }
 void nori_gpu_destroy(nori_gpu_ctx *c) {
     if (!c) return;

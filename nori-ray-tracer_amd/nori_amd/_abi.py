@@ -148,6 +148,8 @@ SIGNATURES = {
                                       C.POINTER(RenderDesc), C.POINTER(C.c_uint32)]),
     "nori_gpu_render_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(RenderDesc), C.c_int, C.c_int,
                                           C.c_void_p, C.POINTER(Stats)]),
+    "nori_gpu_comm_status_word": (C.c_int, [C.c_int, C.c_int]),
+    "nori_gpu_comm_timeout": (C.c_double, [C.c_double, C.c_double, C.c_double]),
 }
 
 COMM_ID_BYTES = 128

@@ -212,16 +212,29 @@ def test_render_modes_agree(built, mode):
     assert_parity(image_parity(gpu, cpu))
 
 
-@pytest.mark.parametrize("bits", ["3", "5"])
-def test_ray_sort_same_image(hfield, bits):
-    """NORI_RAY_SORT (raysort.hip, opt-in): the BVH walks in Morton-sorted
-    order give every ray the same hit, so the film is the unsorted one up to
-    the film sums' order."""
-    s, r, o = hfield
-    base = r.render()
-    os.environ["NORI_RAY_SORT"] = bits
+def test_scan_filter_same_hits(built):
+    """The box-filtered scan (kernels.hip scan_filtered: a lane tests only the
+    triangles whose reference leaf box its ray passes) against the full scan
+    (NORI_SCAN_FILTER=0, read at context creation): the same hit on every
+    ray -- t bit for bit -- and the same image up to the film sums' order."""
+    s = nori_amd.load_scene(scene_path("pa4", "cbox", "cbox_path_mis.xml"), 64, 48, 8)
+    rays = np.concatenate([_rays(30000, 21, [-0.9, 0.05, -0.9], [0.9, 1.5, 0.9]),
+                           _rays(5000, 22, [-3, -1, -3], [3, 3, 6], mint=0.01)])
+    sh = rays.copy()
+    sh[:, 7] = np.random.default_rng(23).uniform(0.01, 2.0, size=sh.shape[0])
+    os.environ["NORI_SCAN_FILTER"] = "0"
     try:
-        srt = r.render()
+        full = nori_amd.GpuRenderer(s, 0)
     finally:
-        os.environ.pop("NORI_RAY_SORT", None)
-    assert np.allclose(base, srt, rtol=1e-5, atol=1e-6), np.abs(base - srt).max()
+        os.environ.pop("NORI_SCAN_FILTER", None)
+    filt = nori_amd.GpuRenderer(s, 0)
+    try:
+        a, b = filt.trace(rays), full.trace(rays)
+        assert np.array_equal(a["t"].view(np.uint32), b["t"].view(np.uint32))
+        assert np.array_equal(a["prim"], b["prim"])
+        assert np.array_equal(filt.trace(sh, any_hit=True)["prim"] >= 0, full.trace(sh, any_hit=True)["prim"] >= 0)
+        fa, fb = filt.render(), full.render()
+        assert np.allclose(fa, fb, rtol=1e-5, atol=1e-6), np.abs(fa - fb).max()
+    finally:
+        filt.close()
+        full.close()

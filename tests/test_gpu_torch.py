@@ -116,11 +116,18 @@ def test_render_sharded_cancel_returns_and_comm_survives(built):
         th = threading.Thread(target=run)
         t0 = time.time()
         th.start()
-        time.sleep(0.15)
+        # cancel once the render is under way (its progress moved), not after
+        # a fixed sleep: a fast device could otherwise finish first
+        while th.is_alive() and not 0.0 < r.progress() < 1.0 and time.time() - t0 < 30:
+            time.sleep(0.002)
+        cancelled_early = th.is_alive()
         r.cancel()
         th.join(timeout=60)
         assert not th.is_alive()
-        assert err and err[0].code == nori_amd._abi.NORI_ERR_CANCELLED, err
+        if cancelled_early and r.progress() < 1.0:
+            assert err and err[0].code == nori_amd._abi.NORI_ERR_CANCELLED, err
+        else:  # the frame was done before the cancel landed: a normal finish
+            assert not err or err[0].code == nori_amd._abi.NORI_ERR_CANCELLED, err
         assert time.time() - t0 < 30
         r.render_sharded(comm, film.data_ptr(), passes=2)
         torch.cuda.synchronize()

@@ -107,3 +107,34 @@ def test_shard_block_lists_are_checked_and_deduplicated(built):
         with pytest.raises(nori_amd.NoriError):
             nd.shard(scene, 0, 2, mode, blocks=[0, nb])
     assert nd.shard(scene, 1, 2, "passes", passes=0)[:2] == (SPP // 2, SPP - SPP // 2)
+
+
+def test_status_word_encoding(built):
+    """The status exchange's word (runtime.hip comm_status_word): severity << 16
+    | rank, reduced by max -- the worst outcome wins and names its rank."""
+    from nori_amd import _abi
+    f = _abi.lib().nori_gpu_comm_status_word
+    assert f(_abi.NORI_OK, 3) == 3
+    assert f(_abi.NORI_ERR_CANCELLED, 5) == (1 << 16) | 5
+    for rc in (_abi.NORI_ERR_INVALID, _abi.NORI_ERR_HIP, _abi.NORI_ERR_OOM, _abi.NORI_ERR_IO):
+        assert f(rc, 7) == (2 << 16) | 7
+    words = [f(_abi.NORI_OK, 0), f(_abi.NORI_ERR_CANCELLED, 1), f(_abi.NORI_OK, 2)]
+    assert max(words) >> 16 == 1 and max(words) & 0xFFFF == 1
+    words.append(f(_abi.NORI_ERR_OOM, 2))
+    assert max(words) >> 16 == 2 and max(words) & 0xFFFF == 2
+    assert f(_abi.NORI_OK, 65535) == 65535
+
+
+def test_comm_timeout_scales_with_the_share(built, monkeypatch):
+    """Watchdog bound of the sharded collectives: max(30 s, 20 x own render
+    time x largest share / own share); 600 s without a share; the env wins."""
+    from nori_amd import _abi
+    monkeypatch.delenv("NORI_COMM_TIMEOUT_S", raising=False)
+    f = _abi.lib().nori_gpu_comm_timeout
+    assert f(0.03, 1e6, 1e6) == 30.0           # a 30 ms frame: the 30 s floor
+    assert f(10.0, 1e6, 1e6) == 200.0          # 20x a 10 s share
+    assert f(10.0, 1e6, 2e6) == 400.0          # a peer holds twice the samples
+    assert f(10.0, 2e6, 1e6) == 200.0          # never below the own share's bound
+    assert f(0.0, 0.0, 1e6) == 600.0           # no share: no own time to scale
+    monkeypatch.setenv("NORI_COMM_TIMEOUT_S", "5")
+    assert f(10.0, 1e6, 1e6) == 5.0
