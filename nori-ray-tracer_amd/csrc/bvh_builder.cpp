@@ -482,18 +482,9 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
         c.ref = me;
         return c;
     };
-    out.leaf_box.assign(6 * (size_t)n, 0.0f);
-    auto set_leaf_box = [&](const RefNode &rn) {
-        for (uint32_t i = rn.b; i < rn.b + rn.a; ++i)
-            for (int k = 0; k < 3; ++k) {
-                out.leaf_box[6 * (size_t)i + k] = rn.box.mn[k];
-                out.leaf_box[6 * (size_t)i + 3 + k] = rn.box.mx[k];
-            }
-    };
     std::function<Child(uint32_t, uint32_t)> emit = [&](uint32_t ri, uint32_t depth) -> Child {
         const RefNode &rn = b.nodes[ri];
         if (rn.leaf) {
-            set_leaf_box(rn);
             Child c = leaf_ref(rn.b, rn.a, depth, 0);
             c.box = rn.box;
             return c;
@@ -516,7 +507,6 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     };
     if (b.nodes[0].leaf) {
         // root leaf: one inner node whose right child box is empty
-        set_leaf_box(b.nodes[0]);
         nodes.resize(16, 0.0f);
         Child l = leaf_ref(b.nodes[0].b, b.nodes[0].a, 1, 0);
         float *nd = &nodes[0];

@@ -74,10 +74,11 @@ struct DevScene {
     uint32_t num_nodes;
     uint32_t num_prims;
     uint32_t num_scan_tris;  // scan mode: prims = triangles (padded to kScanGroup), then spheres
-    // scan mode: triangle filter groups (runtime.hip build_scan_groups), two
-    // float4 each: (min.xyz, scan-index mask bits 0-31) (max.xyz, bits 32-63)
-    const float4 *scan_boxes;
-    uint32_t num_scan_boxes;
+    // scan mode: axis-plane triangle pairs (runtime.hip build_scan_list):
+    // pair g = scan records 2g, 2g+1 in the plane x_a = plane_c[g], pairs of
+    // axis a are [plane_end[a-1], plane_end[a])
+    const float *plane_c;
+    uint32_t plane_end[3];
     float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;
     float invW, invH;

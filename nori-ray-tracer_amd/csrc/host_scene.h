@@ -86,9 +86,6 @@ constexpr uint32_t kLeafMaxPrims = 64;
 struct DeviceBvh {
     std::vector<float> nodes;   // 32 floats per 4-wide node
     std::vector<float> prims;   // 12 floats per primitive
-    // per primitive (leaf order): min.xyz, max.xyz of the reference-tree leaf
-    // holding it -- the box bvh.cpp:420 tests before the leaf's primitives
-    std::vector<float> leaf_box;
     uint32_t num_nodes = 0;
     uint32_t depth = 0;          // max inner-node depth of the 4-wide tree (stack bound: 3 per level)
     uint32_t ref_nodes = 0;      // nodes of the reference-layout tree

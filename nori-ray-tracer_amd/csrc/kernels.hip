@@ -184,15 +184,17 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
 }
 
 // Small scenes: wave-uniform scan of the primitive list.  Every lane tests
-// every primitive in the same order, so the records arrive through scalar
-// loads and no lane diverges; the result is the closest hit (ties: last
-// primitive in scan order wins, as with the reference's `t <= maxt` update,
-// mesh.cpp:119).  The list holds the triangles first, padded with
-// never-hit records to a multiple of kScanGroup so that each group's records
-// come in one batch of scalar loads, then the spheres.  The root box test of
-// bvh.cpp:420 is kept so rays missing the scene never report hits.  K rays
-// per thread share every fetched record.  Expects the adaptive epsilon and
-// rcp already applied by the caller (scan_prologue).
+// every primitive the wave needs in the same order, so the records arrive
+// through scalar loads and no lane diverges; the result is the closest hit.
+// Ties at equal t go to the primitive later in the reference's leaf order
+// (each record's e2.w; the reference visits its leaves in that order and
+// keeps a later equal hit, `t <= maxt`, mesh.cpp:119), so the result does not
+// depend on the order of the list.  The list (runtime.hip build_scan_list):
+// axis-plane triangle pairs by axis, the other triangles padded with
+// never-hit records to a multiple of kScanGroup (one batch of scalar loads
+// per group), then the spheres.  The root box test of bvh.cpp:420 is kept so
+// rays missing the scene never report hits.  K rays per thread share every
+// fetched record.
 template <int K>
 ND void scan_prologue(const DevScene &S, TRay (&r)[K], bool (&live)[K]) {
     const float4 rmn = make_float4(S.root_min[0], S.root_min[1], S.root_min[2], 0.f);
@@ -206,14 +208,96 @@ ND void scan_prologue(const DevScene &S, TRay (&r)[K], bool (&live)[K]) {
         live[k] = live[k] && !(x.maxt < x.mint) && box_test(rmn, rmx, x, tn);
     }
 }
+
+// Can the Moller-Trumbore test of a triangle in the plane x_A = c accept this
+// ray?  `false` is exact: the test then rejects.  With e1_A = e2_A = 0 (both
+// edges in the plane) every product with those zeros drops out of cross() and
+// dot() exactly (device_math.h: x*0 = +-0 and y +- 0 = y), and with
+// T = fl(o_A - c) (tvec_A, of exact sign) and D = d_A what remains is
+//     t's numerator  fl(fl(P' T) - fl(Q' T))   = T n (1 + a),
+//     det            fl(fl(P'' D) - fl(Q'' D))  = -D n (1 + b),
+// where P, Q are the two edge products of the normal component n = P - Q
+// (the primes mark the association; rounding is sign-symmetric) and
+// |a|, |b| <= (2 kappa + 1) u for kappa = (|P| + |Q|) / |P - Q| <= 32,
+// host-checked (runtime.hip axis_plane) with products in the normal range.
+// inv_det = 1/det rounded once (rcp_rn), one more rounding for t, so
+//     t = -(T / D)(1 + e),   |e| <= 132 u < 8e-6 < 2^-16.
+// Hence t >= mint and t <= maxt need T and D of opposite signs and
+// mint (1 - 2^-16) < |T / D| < maxt (1 + 2^-16); the products below carry
+// their own relative rounding (one u each), far inside that margin.  Rays of
+// zero D have det = +-0 (rejected: |det| < 1e-8), and give NaN or 0 here.
+constexpr float kPlaneLo = 1.0f - 0x1p-16f, kPlaneHi = 1.0f + 0x1p-16f;
+ND bool plane_may_hit(float o, float d, float c, float mint, float maxt) {
+    const float T = o - c, ad = fabsf(d);
+    const float s = d > 0.0f ? -T : T;  // > 0: the ray moves towards the plane
+    return s > mint * kPlaneLo * ad && s < maxt * kPlaneHi * ad;
+}
+
+// One triangle record against K rays; the tie rule above.
 template <int K, bool ANY>
+ND void scan_tri(const float4 &a, const float4 &b, const float4 &c, TRay (&r)[K], const bool (&live)[K],
+                 float (&tb)[K], uint32_t (&pb)[K], uint32_t (&lb)[K], float (&ub)[K], float (&vb)[K],
+                 bool (&found)[K]) {
+    const uint32_t pos = __float_as_uint(c.w);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        float t = 0, u = 0, v = 0;
+        const bool h = tri_hit_nb(a, b, c, r[k], t, u, v);  // t <= r.maxt = tb
+        if (h && live[k] && (ANY || t != tb[k] || pos > lb[k])) {
+            found[k] = true;
+            if (!ANY) {
+                r[k].maxt = tb[k] = t;
+                ub[k] = u;
+                vb[k] = v;
+                pb[k] = __float_as_uint(a.w);
+                lb[k] = pos;
+            }
+        }
+    }
+}
+
+// The axis-plane pairs of axis A: a pair is skipped for the whole wave when
+// plane_may_hit is false for every live ray (the current maxt only shrinks,
+// so an earlier bound is never too tight).  CULL false: every pair is tested
+// -- the extension rays of a wave are too incoherent for a wave-wide skip
+// (measured: the checks cost 7 % of the kernel's instructions and skip almost
+// nothing), while shadow rays, short segments towards the lights, skip most
+// walls.
+template <int A, int K, bool ANY, bool CULL>
+ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
+                    uint32_t (&lb)[K], float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
+    const uint32_t g0 = A == 0 ? 0u : S.plane_end[A - 1], g1 = S.plane_end[A];
+    for (uint32_t g = g0; g < g1; ++g) {
+        if (CULL) {
+            const float c = S.plane_c[g];
+            bool may = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const float o = A == 0 ? r[k].o.x : A == 1 ? r[k].o.y : r[k].o.z;
+                const float d = A == 0 ? r[k].d.x : A == 1 ? r[k].d.y : r[k].d.z;
+                may = may || (live[k] && plane_may_hit(o, d, c, r[k].mint, r[k].maxt));
+            }
+            if (!__any(may)) continue;
+        }
+        const float4 *p = S.prims + 6 * (size_t)g;
+        float4 q[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) q[j] = p[j];
+        scan_tri<K, ANY>(q[0], q[1], q[2], r, live, tb, pb, lb, ub, vb, found);
+        scan_tri<K, ANY>(q[3], q[4], q[5], r, live, tb, pb, lb, ub, vb, found);
+    }
+}
+
+template <int K, bool ANY, bool CULL>
 ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                   float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
     scan_prologue<K>(S, r, live);
+    uint32_t lb[K];  // leaf-order position of the closest hit so far
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         tb[k] = INF_F;
         pb[k] = 0xFFFFFFFFu;
+        lb[k] = 0;
         ub[k] = vb[k] = 0.0f;
         found[k] = false;
     }
@@ -223,164 +307,38 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
         for (int k = 0; k < K; ++k) done = done && (found[k] || !live[k]);
         return __all(done);
     };
+    if (S.plane_end[2]) {
+        scan_planes<0, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<1, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<2, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
+    }
     const uint32_t nt = S.num_scan_tris, n = S.num_prims;
-    for (uint32_t i = 0; i < nt; i += kScanGroup) {
+    for (uint32_t i = 2 * S.plane_end[2]; i < nt; i += kScanGroup) {
         if (ANY && all_done()) return;
         const float4 *p = S.prims + 3 * (size_t)i;
         float4 q[3 * kScanGroup];
 #pragma unroll
         for (uint32_t j = 0; j < 3 * kScanGroup; ++j) q[j] = p[j];
 #pragma unroll
-        for (uint32_t g = 0; g < kScanGroup; ++g) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                float t = 0, u = 0, v = 0;
-                bool h = tri_hit_nb(q[3 * g], q[3 * g + 1], q[3 * g + 2], r[k], t, u, v);
-                if (h && live[k]) {
-                    found[k] = true;
-                    if (!ANY) {
-                        r[k].maxt = tb[k] = t;
-                        ub[k] = u;
-                        vb[k] = v;
-                        pb[k] = __float_as_uint(q[3 * g].w);
-                    }
-                }
-            }
-        }
+        for (uint32_t g = 0; g < kScanGroup; ++g)
+            scan_tri<K, ANY>(q[3 * g], q[3 * g + 1], q[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
     for (uint32_t i = nt; i < n; ++i) {
         if (ANY && all_done()) return;
         const float4 *p = S.prims + 3 * (size_t)i;
-        float4 p0 = p[0], p1 = p[1];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float t = 0;
-            bool h = sphere_hit_nb(p0, p1, r[k], t);
-            if (h && live[k]) {
-                found[k] = true;
-                if (!ANY) {
-                    r[k].maxt = tb[k] = t;
-                    ub[k] = vb[k] = 0.0f;
-                    pb[k] = __float_as_uint(p0.w);
-                }
-            }
-        }
-    }
-}
-
-// BoundingBox3f::rayIntersect for a ray whose three reciprocals are finite
-// and non-zero: no slab is NaN unless the origin is, so the swap / max / min
-// steps of bbox.h:336-363 are the plain min and max below and the result is
-// the reference's (a NaN origin, which the reference rejects, may pass here:
-// this is only used to skip work, never to accept a hit).
-ND bool box_lean(const float4 &mn, const float4 &mx, const TRay &r) {
-    const float x1 = (mn.x - r.o.x) * r.rcp.x, x2 = (mx.x - r.o.x) * r.rcp.x;
-    const float y1 = (mn.y - r.o.y) * r.rcp.y, y2 = (mx.y - r.o.y) * r.rcp.y;
-    const float z1 = (mn.z - r.o.z) * r.rcp.z, z2 = (mx.z - r.o.z) * r.rcp.z;
-    const float nearT = fmaxf(fmaxf(fminf(x1, x2), fminf(y1, y2)), fminf(z1, z2));
-    const float farT = fminf(fminf(fmaxf(x1, x2), fmaxf(y1, y2)), fmaxf(z1, z2));
-    return nearT <= farT && r.mint <= farT && nearT <= r.maxt;
-}
-
-// Box-filtered scan of the scan-mode trace kernels (k_extend_scan,
-// k_shadow_scan).  The reference tests a primitive only after the ray has
-// passed the box of the BVH leaf that holds it (bvh.cpp:420-443), with the
-// current maxt, which never exceeds the ray's own.  Slab tests are monotone in
-// the box and in maxt (every step of bbox.h:336-363 rounds monotonically), so
-// a ray that misses a box B containing the leaf box of p, tested with its own
-// [mint, maxt], is never tested against p by the reference, whatever the
-// order of its traversal.  The host pairs the scan's triangles into groups
-// (runtime.hip build_scan_groups) whose B is the union of the members' leaf
-// boxes.  Each lane first tests its ray against every group box (scalar loads,
-// shared by the K rays) and collects the scan indices of the groups it
-// passes; it then runs the exact triangle test on those candidates only, in
-// scan order -- its own loop, so a lane pays for its 1-4 candidates instead
-// of the whole list -- and the spheres by the wave-uniform scan.  Closest hit
-// and ties (the last primitive in scan order wins) are those of scan_core over
-// the candidates, and a triangle left out is one the reference never tests.
-template <int K, bool ANY>
-ND void scan_filtered(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
-                      float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
-    scan_prologue<K>(S, r, live);
-    bool lean = true;  // every live ray's reciprocals finite (no zero direction component)
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        tb[k] = INF_F;
-        pb[k] = 0xFFFFFFFFu;
-        ub[k] = vb[k] = 0.0f;
-        found[k] = false;
-        lean = lean && (!live[k] || (fabsf(r[k].rcp.x) < INF_F && fabsf(r[k].rcp.y) < INF_F && fabsf(r[k].rcp.z) < INF_F));
-    }
-    uint64_t cand[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) cand[k] = 0;
-    const uint32_t ng = S.num_scan_boxes;
-    auto collect = [&](auto test) {
-        for (uint32_t g = 0; g < ng; ++g) {
-            const float4 mn = S.scan_boxes[2 * g], mx = S.scan_boxes[2 * g + 1];
-            const uint64_t gm = (uint64_t)__float_as_uint(mx.w) << 32 | __float_as_uint(mn.w);
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (live[k] && test(mn, mx, r[k])) cand[k] |= gm;
-        }
-    };
-    if (__all(lean)) {
-        collect([](const float4 &mn, const float4 &mx, const TRay &x) { return box_lean(mn, mx, x); });
-    } else {
-        collect([](const float4 &mn, const float4 &mx, const TRay &x) {
-            float tn;
-            return box_test(mn, mx, x, tn);
-        });
-    }
-    // the candidates, lowest scan index first (per lane: divergent loop)
-    for (;;) {
-        bool more = false;
-#pragma unroll
-        for (int k = 0; k < K; ++k) more = more || cand[k] != 0;
-        if (!more) break;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (cand[k] == 0) continue;
-            const uint32_t i = (uint32_t)__builtin_ctzll(cand[k]);
-            cand[k] &= cand[k] - 1;
-            // (plain loads: the tail finisher and the shade kernel pass a
-            // scene whose tables are staged in LDS)
-            const float4 *p = S.prims + 3 * (size_t)i;
-            const float4 a = p[0];
-            float t, u, v;
-            if (tri_hit(a, p[1], p[2], r[k], t, u, v)) {
-                found[k] = true;
-                if (ANY) {
-                    cand[k] = 0;
-                } else {
-                    r[k].maxt = tb[k] = t;
-                    ub[k] = u;
-                    vb[k] = v;
-                    pb[k] = __float_as_uint(a.w);
-                }
-            }
-        }
-    }
-    auto all_done = [&]() {
-        bool done = true;
-#pragma unroll
-        for (int k = 0; k < K; ++k) done = done && (found[k] || !live[k]);
-        return __all(done);
-    };
-    for (uint32_t i = S.num_scan_tris, n = S.num_prims; i < n; ++i) {
-        if (ANY && all_done()) return;
-        const float4 *p = S.prims + 3 * (size_t)i;
         const float4 p0 = p[0], p1 = p[1];
+        const uint32_t pos = __float_as_uint(p[2].w);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float t = 0;
-            const bool h = sphere_hit_nb(p0, p1, r[k], t);
-            if (h && live[k]) {
+            const bool h = sphere_hit_nb(p0, p1, r[k], t);  // t <= r.maxt = tb
+            if (h && live[k] && (ANY || t != tb[k] || pos > lb[k])) {
                 found[k] = true;
                 if (!ANY) {
                     r[k].maxt = tb[k] = t;
                     ub[k] = vb[k] = 0.0f;
                     pb[k] = __float_as_uint(p0.w);
+                    lb[k] = pos;
                 }
             }
         }
@@ -390,12 +348,12 @@ ND void scan_filtered(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&
 // Scan-mode traversal of K rays per thread: every primitive record is
 // fetched once (scalar loads) and tested against K independent rays, which
 // gives the VALU K independent dependency chains to interleave.  Results are
-// those of traverse<0, ANY> ray by ray.
-template <int K, bool ANY>
+// those of traverse<0, ANY> ray by ray.  CULL: the wave-wide plane skips
+// (every caller but the extension kernel, whose waves are incoherent).
+template <int K, bool ANY, bool CULL = true>
 ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                   float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
-    if (S.num_scan_boxes) scan_filtered<K, ANY>(S, r, live, tb, pb, ub, vb, found);
-    else scan_core<K, ANY>(S, r, live, tb, pb, ub, vb, found);
+    scan_core<K, ANY, CULL>(S, r, live, tb, pb, ub, vb, found);
 }
 
 // Primitive records fetched per memory round trip in a BVH leaf.
@@ -761,7 +719,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQue
     float t[K], u[K], v[K];
     uint32_t p[K];
     bool f[K];
-    scan_rays<K, false>(S, r, live, t, p, u, v, f);
+    scan_rays<K, false, false>(S, r, live, t, p, u, v, f);
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (i0 + k * kTraceBlock < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
@@ -1745,7 +1703,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg,
 // scan order wins (the `t <= maxt` update).  A lone tail path then pays one
 // primitive test per ray instead of n.
 struct CoopPrim {  // lane l's primitive, loaded once per finisher wave
-    float4 p0, p1, p2;
+    float4 p0, p1, p2;  // p2.w: leaf-order position (the tie rule of scan_core)
     bool has, tri;
 };
 ND CoopPrim coop_load(const DevScene &S) {
@@ -1795,17 +1753,19 @@ ND bool coop_scan(const DevScene &S, const CoopPrim &cp, const TRay &mine, bool 
             continue;
         }
         if (!hm) continue;
-        // closest hit over the (few) hitting lanes, walked in lane order with
-        // `<=` so that the last primitive among equal t wins; t > 0, so its
-        // bits order like the value and the comparison stays scalar
-        uint32_t best = 0xFFFFFFFFu;
+        // closest hit over the (few) hitting lanes, the later leaf-order
+        // position among equal t (scan_core's rule); t > 0, so its bits order
+        // like the value and the comparison stays scalar
+        uint32_t best = 0xFFFFFFFFu, best_pos = 0;
         int w = 0;
         do {
             const int l = __builtin_ctzll(hm);
             hm &= hm - 1;
             const uint32_t tb = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(tl + 0.0f), l);
-            if (tb <= best) {
+            const uint32_t pos = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(cp.p2.w), l);
+            if (tb < best || (tb == best && pos >= best_pos)) {
                 best = tb;
+                best_pos = pos;
                 w = l;
             }
         } while (hm);
@@ -2616,13 +2576,12 @@ hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue 
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
-    if (stack == 0 && kScanRays > 1) {
+    if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
         return hipGetLastError();
     }
     switch (stack) {
-    case 0: hipLaunchKernelGGL(k_extend<0>, g, b, 0, st, S, q, cnt, G); break;
     case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt, G); break;
     case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, cnt, G); break;
     case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, cnt, G); break;
@@ -2634,13 +2593,12 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
-    if (stack == 0 && kScanRaysShadow > 1) {
+    if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRaysShadow));
         hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, b, 0, st, S, sq, shcnt, rec, G);
         return hipGetLastError();
     }
     switch (stack) {
-    case 0: hipLaunchKernelGGL(k_shadow<0>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec, G); break;

@@ -193,7 +193,7 @@ struct nori_gpu_ctx {
     hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
     nori_camera_desc cam{};
-    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, scan_boxes;
+    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, plane_c;
     DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
     uint32_t spp = 1;    // the scene's sampleCount (default pass count)
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
@@ -372,59 +372,122 @@ void mark_solitary_spheres(const nori_scene_desc &d, const float rmin[3], const 
     }
 }
 
-// Filter groups of the scan-mode trace kernels (kernels.hip scan_filtered):
-// the scan's triangles are paired greedily (each with the unpaired triangle
-// whose leaf box joins its own into the smallest surface area -- the two
-// halves of a wall quad), and a group carries the union of its members'
-// reference leaf boxes and the bit mask of their scan indices, as
-// (min.xyz, mask bits 0-31) (max.xyz, mask bits 32-63).  None when the scan
-// holds more than 64 triangles (a forced scan of a larger scene) or with
-// NORI_SCAN_FILTER=0 (A/B): the kernels then test every primitive.
-template <class IsSphere>
-void build_scan_groups(const DeviceBvh &bvh, uint32_t n, IsSphere is_sphere, uint32_t scan_tris,
-                       std::vector<float> &out) {
-    out.clear();
-    if (const char *e = std::getenv("NORI_SCAN_FILTER"); e && e[0] == '0') return;
-    if (scan_tris > 64) return;
-    struct Item {
-        uint32_t scan;  // index in the scan list
-        float mn[3], mx[3];
-    };
-    std::vector<Item> tris;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (is_sphere(i)) continue;
-        Item it;
-        it.scan = (uint32_t)tris.size();
-        for (int k = 0; k < 3; ++k) it.mn[k] = bvh.leaf_box[6 * (size_t)i + k], it.mx[k] = bvh.leaf_box[6 * (size_t)i + 3 + k];
-        tris.push_back(it);
+// The scan list of scan-mode scenes (kernels.hip scan_core).  Triangles that
+// lie in an axis plane -- both edges with an exactly zero component on the
+// same axis a, so every vertex has x_a = c -- come first, paired by plane:
+// the kernels skip such a pair for a whole wave when no ray of the wave can
+// hit it, a test that is exact only under the conditions checked here (no
+// cancellation in the one remaining product difference of det and of t's
+// numerator, kernels.hip plane_may_hit).  Pairs are ordered by axis (the
+// kernels loop over each axis separately); a plane holding an odd number of
+// triangles pads its last pair with a record no ray hits.  The remaining
+// triangles follow, padded to kScanGroup, then the spheres.  Every record
+// carries its leaf-order position in e2.w: among equal t the scan keeps the
+// hit of the later leaf position, the reference's traversal order.
+bool debug_log();
+struct ScanList {
+    std::vector<float> prims;   // 12 floats per record
+    std::vector<float> plane_c; // per pair: the plane coordinate c
+    uint32_t plane_end[3] = {0, 0, 0};  // pairs with axis <= a
+    uint32_t tris = 0;          // triangle records (pairs + the rest, padded)
+};
+bool axis_plane(const float *r, int a) {
+    const float *e1 = r + 4, *e2 = r + 8;
+    if (e1[a] != 0.0f || e2[a] != 0.0f) return false;
+    const int b = (a + 1) % 3, c = (a + 2) % 3;
+    for (int k : {b, c}) {  // products of normal range: nonzero components in [2^-60, 2^60]
+        for (float x : {e1[k], e2[k]})
+            if (x != 0.0f && !(std::fabs(x) >= 0x1p-60f && std::fabs(x) <= 0x1p60f)) return false;
     }
-    auto join_area = [](const Item &a, const Item &b) {
-        float d[3];
-        for (int k = 0; k < 3; ++k) d[k] = std::max(a.mx[k], b.mx[k]) - std::min(a.mn[k], b.mn[k]);
-        return (double)d[0] * d[1] + (double)d[1] * d[2] + (double)d[2] * d[0];
+    // det and t's numerator are (ray component) x (P - Q) with P, Q the two
+    // products below: kappa = (|P| + |Q|) / |P - Q| bounds their rounding
+    const double P = (double)e1[b] * e2[c], Q = (double)e1[c] * e2[b];
+    const double diff = std::fabs(P - Q);
+    return diff > 0.0 && (std::fabs(P) + std::fabs(Q)) <= 32.0 * diff;
+}
+ScanList build_scan_list(const DeviceBvh &bvh, uint32_t n) {
+    ScanList L;
+    auto rec = [&](uint32_t i) { return &bvh.prims[12 * (size_t)i]; };
+    auto sphere = [&](uint32_t i) {
+        uint32_t f;
+        std::memcpy(&f, rec(i) + 7, 4);
+        return f != 0u;
     };
-    std::vector<char> used(tris.size(), 0);
-    for (size_t a = 0; a < tris.size(); ++a) {
-        if (used[a]) continue;
-        used[a] = 1;
-        int best = -1;
-        double ba = 0;
-        for (size_t b = a + 1; b < tris.size(); ++b)
-            if (!used[b] && (best < 0 || join_area(tris[a], tris[b]) < ba)) best = (int)b, ba = join_area(tris[a], tris[b]);
-        Item g = tris[a];
-        uint64_t mask = 1ull << tris[a].scan;
-        if (best >= 0) {
-            used[(size_t)best] = 1;
-            const Item &o = tris[(size_t)best];
-            for (int k = 0; k < 3; ++k) g.mn[k] = std::min(g.mn[k], o.mn[k]), g.mx[k] = std::max(g.mx[k], o.mx[k]);
-            mask |= 1ull << o.scan;
+    auto add = [&](uint32_t i) {
+        const float *r = rec(i);
+        L.prims.insert(L.prims.end(), r, r + 12);
+        std::memcpy(&L.prims[L.prims.size() - 1], &i, 4);  // e2.w = leaf-order position
+    };
+    auto add_null = [&] {
+        float null_prim[12] = {0};  // zero edges: det = 0, never hit
+        const uint32_t none = 0xFFFFFFFFu;
+        std::memcpy(&null_prim[3], &none, 4);
+        L.prims.insert(L.prims.end(), null_prim, null_prim + 12);
+    };
+    std::vector<int> axis(n, -1);
+    for (uint32_t i = 0; i < n; ++i)
+        if (!sphere(i))
+            for (int a = 0; a < 3 && axis[i] < 0; ++a)
+                if (axis_plane(rec(i), a)) axis[i] = a;
+    for (int a = 0; a < 3; ++a) {
+        // this axis's planes in order of first appearance (leaf order)
+        std::vector<float> planes;
+        for (uint32_t i = 0; i < n; ++i)
+            if (axis[i] == a && std::find(planes.begin(), planes.end(), rec(i)[a]) == planes.end())
+                planes.push_back(rec(i)[a]);
+        for (float c : planes) {
+            uint32_t in_pair = 0;
+            for (uint32_t i = 0; i < n; ++i)
+                if (axis[i] == a && rec(i)[a] == c) {
+                    add(i);
+                    if (++in_pair == 2) {
+                        L.plane_c.push_back(c);
+                        in_pair = 0;
+                    }
+                }
+            if (in_pair) {
+                add_null();
+                L.plane_c.push_back(c);
+            }
         }
-        const uint32_t lo = (uint32_t)mask, hi = (uint32_t)(mask >> 32);
-        float w[2];
-        std::memcpy(&w[0], &lo, 4);
-        std::memcpy(&w[1], &hi, 4);
-        out.insert(out.end(), {g.mn[0], g.mn[1], g.mn[2], w[0], g.mx[0], g.mx[1], g.mx[2], w[1]});
+        L.plane_end[a] = (uint32_t)L.plane_c.size();
     }
+    L.tris = 2 * (uint32_t)L.plane_c.size();
+    uint32_t rest = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (!sphere(i) && axis[i] < 0) add(i), ++rest;
+    for (; rest % kScanGroup; ++rest) add_null();
+    L.tris += rest;
+    for (uint32_t i = 0; i < n; ++i)
+        if (sphere(i)) add(i);
+    if (const char *e = std::getenv("NORI_PLANE_CULL"); e && e[0] == '0') {  // A/B: no plane pairs
+        ScanList F;
+        for (uint32_t i = 0; i < n; ++i)
+            if (!sphere(i)) {
+                const float *r = rec(i);
+                F.prims.insert(F.prims.end(), r, r + 12);
+                std::memcpy(&F.prims[F.prims.size() - 1], &i, 4);
+                ++F.tris;
+            }
+        for (; F.tris % kScanGroup; ++F.tris) {
+            float null_prim[12] = {0};
+            const uint32_t none = 0xFFFFFFFFu;
+            std::memcpy(&null_prim[3], &none, 4);
+            F.prims.insert(F.prims.end(), null_prim, null_prim + 12);
+        }
+        for (uint32_t i = 0; i < n; ++i)
+            if (sphere(i)) {
+                const float *r = rec(i);
+                F.prims.insert(F.prims.end(), r, r + 12);
+                std::memcpy(&F.prims[F.prims.size() - 1], &i, 4);
+            }
+        return F;
+    }
+    if (debug_log())
+        std::fprintf(stderr, "[nori] scan list: %zu axis-plane pairs (x %u, y %u, z %u), %u other triangle records\n",
+                     L.plane_c.size(), L.plane_end[0], L.plane_end[1] - L.plane_end[0],
+                     L.plane_end[2] - L.plane_end[1], rest);
+    return L;
 }
 
 // The path kernels' lite variants (FULL = false) serve scenes made of the
@@ -654,34 +717,9 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     if (mode && std::string(mode) == "bvh") scan = false;
     if (mode && std::string(mode) == "scan") scan = true;
     if (scan) c.stack = 0;
-    // scan order: triangles (leaf order) padded to kScanGroup with records no
-    // ray hits (zero edges: det = 0, or NaN t), then spheres (leaf order)
-    std::vector<float> scan_prims;
-    std::vector<float> scan_boxes;  // filter groups of the scan kernels: (min, mask lo) (max, mask hi)
-    uint32_t scan_tris = 0;
-    if (scan) {
-        auto is_sphere = [&](uint32_t i) {
-            uint32_t f;
-            std::memcpy(&f, &bvh.prims[12 * (size_t)i + 7], 4);
-            return f != 0u;
-        };
-        auto add = [&](uint32_t i) {
-            scan_prims.insert(scan_prims.end(), bvh.prims.begin() + 12 * (size_t)i, bvh.prims.begin() + 12 * (size_t)i + 12);
-        };
-        for (uint32_t i = 0; i < off; ++i)
-            if (!is_sphere(i)) add(i), ++scan_tris;
-        while (scan_tris % kScanGroup) {
-            float null_prim[12] = {0};
-            const uint32_t none = 0xFFFFFFFFu;
-            std::memcpy(&null_prim[3], &none, 4);
-            scan_prims.insert(scan_prims.end(), null_prim, null_prim + 12);
-            ++scan_tris;
-        }
-        for (uint32_t i = 0; i < off; ++i)
-            if (is_sphere(i)) add(i);
-        build_scan_groups(bvh, off, is_sphere, scan_tris, scan_boxes);
-    }
-    const std::vector<float> &prim_list = scan ? scan_prims : bvh.prims;
+    ScanList scan_list;
+    if (scan) scan_list = build_scan_list(bvh, off);
+    const std::vector<float> &prim_list = scan ? scan_list.prims : bvh.prims;
 
     std::vector<float> pos(4 * (size_t)d.num_vertices), nrm(4 * (size_t)d.num_vertices);
     for (uint32_t v = 0; v < d.num_vertices; ++v) {
@@ -697,7 +735,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     if (cdf.empty()) cdf.assign(1, 0.0f);
     c.nodes.upload(bvh.nodes);
     c.prims.upload(prim_list);
-    if (!scan_boxes.empty()) c.scan_boxes.upload(scan_boxes);
+    if (!scan_list.plane_c.empty()) c.plane_c.upload(scan_list.plane_c);
     c.tri_vidx.upload(tri_vidx);
     c.pos.upload(pos);
     c.nrm.upload(nrm);
@@ -747,9 +785,9 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.num_emitters = d.num_emitters;
     S.num_nodes = bvh.num_nodes;
     S.num_prims = (uint32_t)(prim_list.size() / 12);
-    S.num_scan_tris = scan_tris;
-    S.scan_boxes = scan_boxes.empty() ? nullptr : c.scan_boxes.as<float4>();
-    S.num_scan_boxes = (uint32_t)(scan_boxes.size() / 8);
+    S.num_scan_tris = scan_list.tris;
+    S.plane_c = scan_list.plane_c.empty() ? nullptr : c.plane_c.as<float>();
+    for (int a = 0; a < 3; ++a) S.plane_end[a] = scan_list.plane_end[a];
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     S.blob = use_blob ? c.blob.as<float4>() : nullptr;
     S.blob_bytes = use_blob ? (uint32_t)blob.size() : 0u;

@@ -163,8 +163,12 @@ def variance_gray(var_rgb):
     weight -- then divided by 255.  OpenCV's 8-bit grey conversion is fixed
     point: (4899 c0 + 9617 c1 + 1868 c2 + 2^13) >> 14.  (OpenCV is not in
     this image: this step is a restatement, unpinned.)"""
-    b = ldr_bytes(var_rgb).astype(np.int64)
-    bgr = b[..., ::-1]
+    return variance_gray_bytes(ldr_bytes(var_rgb))
+
+
+def variance_gray_bytes(rgb8):
+    """variance_gray() of an 8-bit RGB image as stored in a PNG (H, W, 3)."""
+    bgr = np.asarray(rgb8).astype(np.int64)[..., ::-1]
     gray = (4899 * bgr[..., 0] + 9617 * bgr[..., 1] + 1868 * bgr[..., 2] + (1 << 13)) >> 14
     return (gray.astype(np.float64) / 255.0).astype(np.float32)
 

@@ -92,3 +92,18 @@ def test_denoise_cli(built, tmp_path):
     out = nori_amd.read_exr(str(tmp_path / "c_denoised.exr"))
     var = nori_amd.variance_gray(nori_amd.film_variance(s, stats))
     assert np.allclose(out, nori_amd.denoise(img, var), rtol=1e-6, atol=1e-7)
+
+
+def test_denoise_reproduces_reference_final_denoised(built):
+    """nori_denoise (mode 0, the script's parameters) on the reference's
+    final.png + final_variance.png against the reference's final_denoised.png:
+    >= 99.99 % of the bytes equal and none off by more than 1 LSB (fp32 in the
+    kernel against the script's float64)."""
+    from test_denoise import compare_bytes, reference_triple
+
+    img, var, ref = reference_triple("final", "final_variance", "final_denoised")
+    out = nori_amd.denoise(img.astype(np.float32), var.astype(np.float32), radius=3, patch=3, k=0.02, mode=0,
+                           script_scale=False)
+    exact, dmax, _ = compare_bytes(out, ref)
+    print(f"final_denoised: {exact * 100:.4f} % equal bytes, max {dmax} LSB")
+    assert exact >= 0.9999 and dmax <= 1, (exact, dmax)

@@ -212,26 +212,41 @@ def test_render_modes_agree(built, mode):
     assert_parity(image_parity(gpu, cpu))
 
 
-def test_scan_filter_same_hits(built):
-    """The box-filtered scan (kernels.hip scan_filtered: a lane tests only the
-    triangles whose reference leaf box its ray passes) against the full scan
-    (NORI_SCAN_FILTER=0, read at context creation): the same hit on every
-    ray -- t bit for bit -- and the same image up to the film sums' order."""
+def test_plane_cull_same_hits(built):
+    """The scan's exact axis-plane culls (kernels.hip plane_may_hit: a wave
+    skips a wall pair that no ray of it can hit) against the scan without
+    them (NORI_PLANE_CULL=0, read at context creation): the same hit on every
+    ray -- t bit for bit -- and the same image up to the film sums' order.
+    Rays include grazing ones (direction components of 1e-7 .. 1e-3 towards
+    the walls) and origins on the wall planes."""
     s = nori_amd.load_scene(scene_path("pa4", "cbox", "cbox_path_mis.xml"), 64, 48, 8)
     rays = np.concatenate([_rays(30000, 21, [-0.9, 0.05, -0.9], [0.9, 1.5, 0.9]),
                            _rays(5000, 22, [-3, -1, -3], [3, 3, 6], mint=0.01)])
+    rng = np.random.default_rng(24)
+    graze = _rays(20000, 25, [-0.9, 0.05, -0.9], [0.9, 1.5, 0.9])
+    ax = rng.integers(0, 3, graze.shape[0])
+    graze[np.arange(graze.shape[0]), 4 + ax] = (rng.choice([-1, 1], graze.shape[0]) *
+                                                10.0 ** rng.uniform(-7, -3, graze.shape[0]))
+    on = graze[:10000].copy()  # origins on the wall planes y = 0, y = 1.59, x = 1, z = -1.04
+    which = rng.integers(0, 4, on.shape[0])
+    on[which == 0, 1] = 0.0
+    on[which == 1, 1] = 1.59
+    on[which == 2, 0] = 1.0
+    on[which == 3, 2] = -1.04
+    rays = np.concatenate([rays, graze, on]).astype(np.float32)
     sh = rays.copy()
     sh[:, 7] = np.random.default_rng(23).uniform(0.01, 2.0, size=sh.shape[0])
-    os.environ["NORI_SCAN_FILTER"] = "0"
+    os.environ["NORI_PLANE_CULL"] = "0"
     try:
         full = nori_amd.GpuRenderer(s, 0)
     finally:
-        os.environ.pop("NORI_SCAN_FILTER", None)
+        os.environ.pop("NORI_PLANE_CULL", None)
     filt = nori_amd.GpuRenderer(s, 0)
     try:
         a, b = filt.trace(rays), full.trace(rays)
         assert np.array_equal(a["t"].view(np.uint32), b["t"].view(np.uint32))
         assert np.array_equal(a["prim"], b["prim"])
+        assert np.array_equal(a["u"].view(np.uint32), b["u"].view(np.uint32))
         assert np.array_equal(filt.trace(sh, any_hit=True)["prim"] >= 0, full.trace(sh, any_hit=True)["prim"] >= 0)
         fa, fb = filt.render(), full.render()
         assert np.allclose(fa, fb, rtol=1e-5, atol=1e-6), np.abs(fa - fb).max()
