@@ -128,7 +128,7 @@ def profiled(prefix, config="c2"):
         return None
     for k, v in d.get("kernels", {}).items():
         if k.startswith(prefix):
-            return dict(v, name=k)
+            return dict(v, name=k, file=f"profiles/{name}", commit=d.get("commit"))
     return None
 
 
@@ -163,13 +163,15 @@ def roofline(ts, samples, config="c2"):
         if prof:
             row["traffic_bytes_per_launch"] = prof.get("hbm_bytes_per_launch")
             row["rocprof_avg_launch_ms"] = prof.get("trace_avg_ms")
+            # the counters come from the committed profile, collected at this commit
+            row["profile"] = {"file": prof["file"], "commit": prof.get("commit"), "kernel": prof["name"]}
             if prof.get("sq_insts_valu_per_launch") and prof.get("trace_avg_ms"):
                 rate = prof["sq_insts_valu_per_launch"] * 64 / (prof["trace_avg_ms"] / 1e3)
                 row["valu_issue_frac"] = rate / VALU_PEAK
         rows[name] = row
     d = rows["k_extend"]
     return {"bound": "hbm", "kernel": "k_extend", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": d["frac"], "traffic": d.get("traffic_bytes_per_launch"),
+            "unit": "GB/s", "frac": d["frac"], "traffic": d.get("traffic_bytes_per_launch"), "traffic_profile": d.get("profile"),
             "bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": d["avg_launch_ms"], "launches": launches,
             "measured": "HIP events on the launch stream, one extra render after the timed region with one pool "
                         "part (NORI_POOL_PARTS=1): kernels serialised on one stream",

@@ -23,64 +23,6 @@
 namespace nori {
 namespace {
 
-#if NORI_BVH_QUANT
-// Quantized 4-wide nodes (64 B instead of 128 B): per axis, an origin (the
-// union box's minimum) and a power-of-two step s with 255 s >= the union's
-// extent; each child bound is an 8-bit multiple of s, rounded outward and
-// checked with the device's own decode, origin + (float)q * s (exact product,
-// one rounding), so every decoded child box contains the exact one.  The
-// candidate primitives of a ray are a superset of the exact boxes' (the
-// closest hit is unchanged); unused children get q_lo = 255 > q_hi = 0.
-// Layout (16 words): origin.xyz, s.x | s.y, s.z, lo.x[4], lo.y[4] |
-// lo.z[4], hi.x[4], hi.y[4], hi.z[4] | ref[4]   (byte i = child i).
-float qdec(float o, uint32_t q, float s) { return o + (float)q * s; }  // == kernels.hip qdec
-void quantize_nodes(std::vector<float> &nodes, uint32_t n) {
-    std::vector<float> qn(16 * (size_t)n, 0.0f);
-    for (uint32_t j = 0; j < n; ++j) {
-        const float *nd = &nodes[32 * (size_t)j];
-        bool used[4];
-        float org[3], s[3];
-        uint32_t lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-        for (int i = 0; i < 4; ++i) used[i] = !std::isnan(nd[i]);
-        for (int k = 0; k < 3; ++k) {
-            float mn = __builtin_inff(), mx = -__builtin_inff();
-            for (int i = 0; i < 4; ++i)
-                if (used[i]) mn = std::fmin(mn, nd[4 * k + i]), mx = std::fmax(mx, nd[4 * (3 + k) + i]);
-            if (!(mn <= mx)) mn = mx = 0.0f;  // no used child
-            const double ext = (double)mx - (double)mn;
-            int e = -100;
-            if (ext > 0) e = std::max(-100, (int)std::ceil(std::log2(ext / 255.0)));
-            while (255.0 * std::ldexp(1.0, e) < ext) ++e;
-            org[k] = mn;
-            s[k] = std::ldexp(1.0f, e);
-            for (int i = 0; i < 4; ++i) {
-                uint32_t ql = 255, qh = 0;
-                if (used[i]) {
-                    const float cmn = nd[4 * k + i], cmx = nd[4 * (3 + k) + i];
-                    double a = std::floor(((double)cmn - mn) / s[k]), b = std::ceil(((double)cmx - mn) / s[k]);
-                    ql = (uint32_t)std::min(255.0, std::max(0.0, a));
-                    qh = (uint32_t)std::min(255.0, std::max(0.0, b));
-                    while (ql > 0 && qdec(org[k], ql, s[k]) > cmn) --ql;
-                    while (qh < 255 && qdec(org[k], qh, s[k]) < cmx) ++qh;
-                }
-                lo[k] |= ql << (8 * i);
-                hi[k] |= qh << (8 * i);
-            }
-        }
-        float *q = &qn[16 * (size_t)j];
-        q[0] = org[0], q[1] = org[1], q[2] = org[2], q[3] = s[0];
-        q[4] = s[1], q[5] = s[2];
-        std::memcpy(&q[6], &lo[0], 4);
-        std::memcpy(&q[7], &lo[1], 4);
-        std::memcpy(&q[8], &lo[2], 4);
-        std::memcpy(&q[9], &hi[0], 4);
-        std::memcpy(&q[10], &hi[1], 4);
-        std::memcpy(&q[11], &hi[2], 4);
-        std::memcpy(&q[12], &nd[24], 16);  // child refs
-    }
-    nodes.swap(qn);
-}
-#endif
 
 struct Box {
     float mn[3], mx[3];
@@ -583,9 +525,6 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     out.num_nodes = (uint32_t)(nodes.size() / 32);
     out.depth = depth4;
     (void)max_depth;
-#if NORI_BVH_QUANT
-    quantize_nodes(nodes, out.num_nodes);
-#endif
     lap("device layout");
 }
 

@@ -172,9 +172,6 @@ struct ShadowQueue {
 // static stream of 256-id chunks (consecutive ids = adjacent pixels of one
 // 32x32 block, so a segment traces coherent camera rays).
 constexpr uint32_t kSeg = 256;
-#ifndef NORI_BVH_QUANT  // quantized 64-byte BVH nodes (same default as host_scene.h)
-#define NORI_BVH_QUANT 0
-#endif
 #ifndef NORI_SCAN_GROUP
 #define NORI_SCAN_GROUP 4
 #endif

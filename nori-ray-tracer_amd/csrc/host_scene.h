@@ -9,15 +9,6 @@
 
 #include "../../include/nori_gpu.h"
 
-// 1: quantized 64-byte BVH nodes (bvh_builder.cpp quantize_nodes), 0: exact
-// 128-byte nodes (default: the quantized nodes measured 9-12 % slower on C3
-// and the table scene -- the traversal is latency/VALU-bound, not bound by
-// node bytes).  The same default is in dev_scene.h (the kernels' side);
-// a build that overrides it passes -DNORI_BVH_QUANT to both compilers.
-#ifndef NORI_BVH_QUANT
-#define NORI_BVH_QUANT 0
-#endif
-
 namespace nori {
 
 // NoriException (common.h:150-155) carrying the C-ABI status code.

@@ -95,3 +95,48 @@ def test_cull_implies_reject(built):
         culled += int((~may).sum())
         checked += len(o)
     assert culled > checked // 4  # the cull is not vacuous
+
+
+def moller_trumbore_plane(p0, e1, e2, o, d, mint, maxt, A):
+    """kernels.hip tri_hit_plane<A>: the products with the zero components left out."""
+    with np.errstate(all="ignore"):
+        tv = (o[0] - p0[0], o[1] - p0[1], o[2] - p0[2])
+        if A == 0:
+            pv = (d[1] * e2[2] - d[2] * e2[1], -(d[0] * e2[2]), d[0] * e2[1])
+            det = e1[1] * pv[1] + e1[2] * pv[2]
+            qv = (tv[1] * e1[2] - tv[2] * e1[1], -(tv[0] * e1[2]), tv[0] * e1[1])
+            tn = e2[1] * qv[1] + e2[2] * qv[2]
+        elif A == 1:
+            pv = (d[1] * e2[2], d[2] * e2[0] - d[0] * e2[2], -(d[1] * e2[0]))
+            det = e1[0] * pv[0] + e1[2] * pv[2]
+            qv = (tv[1] * e1[2], tv[2] * e1[0] - tv[0] * e1[2], -(tv[1] * e1[0]))
+            tn = e2[0] * qv[0] + e2[2] * qv[2]
+        else:
+            pv = (-(d[2] * e2[1]), d[2] * e2[0], d[0] * e2[1] - d[1] * e2[0])
+            det = e1[0] * pv[0] + e1[1] * pv[1]
+            qv = (-(tv[2] * e1[1]), tv[2] * e1[0], tv[0] * e1[1] - tv[1] * e1[0])
+            tn = e2[0] * qv[0] + e2[1] * qv[1]
+        inv = f32(1) / det
+        u = dot(tv, pv) * inv
+        v = dot(d, qv) * inv
+        t = tn * inv
+        ok = (~((det > f32(-1e-8)) & (det < f32(1e-8))) & ~((u < 0) | (u > 1)) & ~((v < 0) | (u + v > 1)) &
+              (t >= mint) & (t <= maxt))
+        return ok, t, u, v
+
+
+def test_plane_test_is_the_generic_test(built):
+    """tri_hit_plane<A> accepts exactly the rays tri_hit_nb accepts, with the
+    same t bits and the same u, v values (up to the sign of a zero)."""
+    rng = np.random.default_rng(11)
+    for p0, e1, e2, a in plane_triangles():
+        o, d = rays(rng, 200000)
+        o[:40000, a] = p0[a]
+        mint = np.maximum(f32(1e-4), f32(1e-4) * np.abs(o).max(axis=1)).astype(f32)
+        maxt = np.full(len(o), np.inf, f32)
+        O, D = (o[:, 0], o[:, 1], o[:, 2]), (d[:, 0], d[:, 1], d[:, 2])
+        h1, t1 = moller_trumbore(p0, e1, e2, O, D, mint, maxt)
+        h2, t2, u2, v2 = moller_trumbore_plane(p0, e1, e2, O, D, mint, maxt, a)
+        assert np.array_equal(h1, h2)
+        assert np.array_equal(t1[h1].view(np.uint32), t2[h2].view(np.uint32))
+        assert h1.sum() > 100
