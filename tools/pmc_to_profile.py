@@ -40,11 +40,13 @@ def per_kernel(path, counter):
 def main():
     tag = sys.argv[1]
     import subprocess
-    try:
-        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
-                                text=True).stdout.strip()
-    except OSError:
-        commit = None
+    commit = os.environ.get("NORI_PROFILE_COMMIT")  # set when summarising on the GPU box (no .git there)
+    if not commit:
+        try:
+            commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                    text=True).stdout.strip() or None
+        except OSError:
+            commit = None
     out = {"tag": tag, "commit": commit, "method": "rocprofv3 --pmc FETCH_SIZE (pass 1) / WRITE_SIZE (pass 2) --kernel-trace; "
                                   "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH correction)",
            "kernels": {}}
