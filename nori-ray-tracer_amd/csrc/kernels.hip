@@ -2417,11 +2417,14 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
     uint32_t inval = 0;
     for (int j = threadIdx.x; j < npix; j += kSplatBlock) {
         const int ly = j / bw, lx = j - ly * bw, x = ox + lx, y = oy + ly;
-        float acc[K][K][4];
+        // the window's RGBW sums as two packed pairs per cell (RG, BW): each
+        // half of a v_pk_mul_f32 / v_pk_add_f32 rounds as the scalar op does
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 acc[K][K][2];
 #pragma unroll
         for (int a = 0; a < K; ++a)
 #pragma unroll
-            for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = acc[a][c][2] = acc[a][c][3] = 0.0f;
+            for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = f2{0.0f, 0.0f};
         bool any = false;
         float vs[7] = {0, 0, 0, 0, 0, 0, 0};  // sample statistics of the pixel (sd.var)
         // the next NORI_SPLAT_DEPTH passes' records are in flight while this one is splatted
@@ -2466,21 +2469,18 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
                 wx[d] = (cx >= x0 && cx <= x1) ? fx : 0.0f;
                 wy[d] = (cy >= y0 && cy <= y1) ? fy : 0.0f;
             }
-            float lx_[K], ly_[K], lz_[K];  // Color4f(value) * wx (the row factor is shared by all rows)
+            f2 lrg[K], lbw[K];  // Color4f(value) * wx (the row factor is shared by all rows)
 #pragma unroll
             for (int c = 0; c < K; ++c) {
-                lx_[c] = L.x * wx[c];
-                ly_[c] = L.y * wx[c];
-                lz_[c] = L.z * wx[c];
+                lrg[c] = f2{L.x, L.y} * wx[c];
+                lbw[c] = f2{L.z, 1.0f} * wx[c];  // (1 * wx) = wx exactly
             }
 #pragma unroll
             for (int a = 0; a < K; ++a)
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    acc[a][c][0] += lx_[c] * wy[a];
-                    acc[a][c][1] += ly_[c] * wy[a];
-                    acc[a][c][2] += lz_[c] * wy[a];
-                    acc[a][c][3] += wx[c] * wy[a];  // (1 * wx) * wy
+                    acc[a][c][0] += lrg[c] * wy[a];
+                    acc[a][c][1] += lbw[c] * wy[a];
                 }
         }
         if (any && sd.var) {
@@ -2493,11 +2493,12 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
                     float *t = tile + 4 * ((ly + a) * TS + (lx + c));
-                    if (acc[a][c][3] != 0.0f || acc[a][c][0] != 0.0f || acc[a][c][1] != 0.0f || acc[a][c][2] != 0.0f) {
-                        atomicAdd(t + 0, acc[a][c][0]);
-                        atomicAdd(t + 1, acc[a][c][1]);
-                        atomicAdd(t + 2, acc[a][c][2]);
-                        atomicAdd(t + 3, acc[a][c][3]);
+                    const f2 rg = acc[a][c][0], bw = acc[a][c][1];
+                    if (bw.y != 0.0f || rg.x != 0.0f || rg.y != 0.0f || bw.x != 0.0f) {
+                        atomicAdd(t + 0, rg.x);
+                        atomicAdd(t + 1, rg.y);
+                        atomicAdd(t + 2, bw.x);
+                        atomicAdd(t + 3, bw.y);
                     }
                 }
         }
