@@ -27,6 +27,8 @@
  *   nori_film_variance    <- renderScene's variance image src/render.cpp:164-169,190-245
  *   nori_denoise          <- denoiser/denoiser.py:53-66 (NL-means)
  *   nori_scene_bvh_info   <- BVH::build/statistics        src/bvh.cpp:329-402
+ *   nori_scene_scan_list  (introspection: the small-scene scan list and its
+ *                          exact in-plane filters, for the CPU tests)
  *   nori_gpu_comm_*, nori_gpu_render_sharded
  *                         <- the same pass loop spread over the GPUs of a node,
  *                            one process per GPU; the cross-GPU film merge is
@@ -285,6 +287,23 @@ typedef struct nori_bvh_info {
 } nori_bvh_info;
 int nori_scene_bvh_info(const nori_scene_desc *scene, nori_bvh_info *out);
 
+/* Host-side scan list of a small scene (<= 64 primitives) exactly as
+ * nori_gpu_create builds it (no device needed; introspection for tests -- no
+ * reference counterpart): the primitive records in scan order (12 floats
+ * each: v0 | prim id, e1 | sphere flag, e2 | leaf position; a sphere is
+ * (centre | id, radius, ...)), per axis-plane pair the plane coordinate and
+ * the in-plane filter of the binned extension kernel (8 floats: mid_B,
+ * half_B + Kb, mid_C, half_C + Kb, Ka, c, 0, 0).  Call with null arrays for
+ * the counts; records = 0 for a BVH scene. */
+typedef struct nori_scan_info {
+    uint32_t records;       /* 12-float records (pairs, other triangles padded, spheres) */
+    uint32_t pairs;         /* axis-plane pairs: records 2g, 2g+1                          */
+    uint32_t plane_end[3];  /* pairs of axis <= a                                          */
+    uint32_t tris;          /* triangle records                                            */
+} nori_scan_info;
+int nori_scene_scan_list(const nori_scene_desc *scene, nori_scan_info *info, float *records, float *plane_c,
+                         float *plane_f);
+
 /* ---- GPU context ----------------------------------------------------------- */
 typedef struct nori_gpu_ctx nori_gpu_ctx;
 
@@ -392,11 +411,12 @@ int nori_gpu_shard_desc(const nori_scene_desc *scene, const nori_gpu_render_desc
  * whose device faulted (a sticky HIP error) cannot join: it aborts the
  * communicator (ncclCommAbort) and returns NORI_ERR_HIP.  Its peers, and any
  * rank whose peers do not reach a collective, give up after the watchdog
- * bound nori_gpu_comm_timeout(own render seconds, own samples, largest
- * share's samples) -- max(30 s, 20 x the own render time scaled to the
- * largest share), 600 s for a rank without a share, NORI_COMM_TIMEOUT_S
- * seconds if set -- abort and return NORI_ERR_HIP; an aborted communicator
- * fails every later call. */
+ * bound nori_gpu_comm_timeout(own status, own render seconds, own samples,
+ * largest share's samples) -- max(30 s, 20 x the own render time scaled to
+ * the largest share) after a rendered share, 600 s for a rank whose share
+ * failed, was cancelled or is empty, NORI_COMM_TIMEOUT_S seconds if set --
+ * abort and return NORI_ERR_HIP; an aborted communicator fails every later
+ * call. */
 int nori_gpu_render_sharded(nori_gpu_ctx *ctx, nori_gpu_comm *comm, const nori_gpu_render_desc *desc, int mode,
                             int root, float *film_dev, nori_gpu_stats *stats);
 /* The status word a rank contributes to the exchange (reduced by max):
@@ -404,8 +424,9 @@ int nori_gpu_render_sharded(nori_gpu_ctx *ctx, nori_gpu_comm *comm, const nori_g
  * 2 for any other status.  Pure function. */
 int nori_gpu_comm_status_word(int status, int rank);
 /* The watchdog bound of a sharded render's collectives, in seconds (see
- * nori_gpu_render_sharded).  Pure function (reads NORI_COMM_TIMEOUT_S). */
-double nori_gpu_comm_timeout(double own_seconds, double own_samples, double max_samples);
+ * nori_gpu_render_sharded); status = the rank's own share's outcome.  Pure
+ * function (reads NORI_COMM_TIMEOUT_S). */
+double nori_gpu_comm_timeout(int status, double own_seconds, double own_samples, double max_samples);
 
 #ifdef __cplusplus
 }

@@ -78,6 +78,8 @@ struct DevScene {
     // pair g = scan records 2g, 2g+1 in the plane x_a = plane_c[g], pairs of
     // axis a are [plane_end[a-1], plane_end[a])
     const float *plane_c;
+    // per pair: the in-plane filter of k_extend_bin (runtime.hip plane_filters)
+    const float4 *plane_f;
     uint32_t plane_end[3];
     float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;

@@ -20,6 +20,8 @@
 // (bvh.cpp:404-462) and ImageBlock::put (block.cpp:93-133).
 #include "kernels.h"
 
+#include <cstdlib>
+
 // The kernels are compiled in three translation units so that hipcc builds
 // them in parallel: NORI_TU 0 (this file) = everything but the two largest
 // groups, 1 (kernels_shade.hip) = k_shade + launch_shade, 2
@@ -229,11 +231,15 @@ ND void scan_prologue(const DevScene &S, TRay (&r)[K], bool (&live)[K]) {
 // mint (1 - 2^-16) < |T / D| < maxt (1 + 2^-16); the products below carry
 // their own relative rounding (one u each), far inside that margin.  Rays of
 // zero D have det = +-0 (rejected: |det| < 1e-8), and give NaN or 0 here.
+// The bounds assume mint > 0 and maxt > 0 (every path ray); a trace-API ray
+// with mint <= 0 (Moller-Trumbore then accepts t = +-0 on the plane) or
+// maxt <= 0 drops the bound on that side.
 constexpr float kPlaneLo = 1.0f - 0x1p-16f, kPlaneHi = 1.0f + 0x1p-16f;
 ND bool plane_may_hit(float o, float d, float c, float mint, float maxt) {
     const float T = o - c, ad = fabsf(d);
     const float s = d > 0.0f ? -T : T;  // > 0: the ray moves towards the plane
-    return s > mint * kPlaneLo * ad && s < maxt * kPlaneHi * ad;
+    const float lo = mint > 0.0f ? mint * kPlaneLo * ad : -INF_F, hi = maxt > 0.0f ? maxt * kPlaneHi * ad : INF_F;
+    return s > lo && s < hi;
 }
 
 // One triangle record against K rays; the tie rule above.  PLANE 0-2: an
@@ -763,6 +769,209 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
     for (int k = 0; k < K; ++k)
         if (valid[k] && !f[k]) shadow_add(rec, c[k]);
 }
+
+// ------------------------------------------------------------------ binned extension scan
+// k_extend_scan tests every axis-plane pair against every ray; a ray inside
+// the Cornell box can be accepted by one wall (where it leaves the box), so
+// most of those tests are wasted, yet a 64-ray wave always holds some ray for
+// every wall.  k_extend_bin therefore moves the pair tests out of the ray's
+// lane: (1) every lane filters its ray against each pair -- a dozen VALU
+// instructions (pair_candidate, exact: runtime.hip plane_filters) -- and
+// hands the (ray, pair) candidates to a work-group list in LDS, while it
+// scans the remaining triangles and the spheres itself as before; (2) the
+// work-group's four waves run the listed candidates 64 at a time, each lane
+// one (ray, pair) with the pair's two records and the ray read from LDS --
+// dense lanes whatever pair they belong to; (3) every lane merges its
+// candidates' results into its own closest hit.  The tie rule of scan_core
+// (closest t, then the later leaf position) makes the result independent of
+// the order of the tests, so the hits are those of k_extend_scan bit for bit
+// (NORI_EXTEND_CHECK compares the two on every launch).  A ray with more
+// than kBinSlots candidate pairs tests every pair in its own lane.
+#ifndef NORI_EXTEND_BIN
+#define NORI_EXTEND_BIN 1
+#endif
+constexpr int kBinBlock = 256;
+constexpr uint32_t kBinSlices = kTraceGroup * kSeg / kBinBlock;  // work-groups per group of segments
+constexpr int kBinSlots = 2;
+constexpr uint32_t kBinMaxPairs = 32;
+template <int A>
+ND float comp(const V3 &v) { return A == 0 ? v.x : A == 1 ? v.y : v.z; }
+
+// May the Moller-Trumbore test of a triangle of this pair accept the ray?
+// false is exact (runtime.hip plane_filters): the crossing t_f must lie in
+// [mint, maxt] up to the plane_may_hit margins (|t_f / t - 1| <= gamma_3 on
+// top of its 133 u), and its in-plane point within the widened rectangle.
+// NaN and infinite crossings (d_A = 0: det = 0, never accepted) fail the
+// range test or pass the rectangle test, never wrongly reject.
+template <int A>
+ND bool pair_candidate(const TRay &r, const float4 &f0, const float4 &f1, float mlo, float mhi, float so, float sd) {
+    constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+    const float tf = (f1.y - comp<A>(r.o)) * comp<A>(r.rcp);
+    const float dB = __builtin_fmaf(tf, comp<B>(r.d), comp<B>(r.o) - f0.x);
+    const float dC = __builtin_fmaf(tf, comp<C>(r.d), comp<C>(r.o) - f0.z);
+    const float S = __builtin_fmaf(fabsf(tf), sd, so);
+    const float thB = __builtin_fmaf(f1.x, S, f0.y), thC = __builtin_fmaf(f1.x, S, f0.w);
+    return tf > mlo && tf <= mhi && !(fabsf(dB) > thB) && !(fabsf(dC) > thC);
+}
+
+// This ray's candidate pairs of axis A: the count and the first kBinSlots
+// pair indices (5 bits each, 8 bits apart).
+template <int A>
+ND void bin_axis(const DevScene &S, const TRay &r, bool live, float mlo, float mhi, uint32_t &nc, uint32_t &cand) {
+    constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+    const uint32_t g0 = A == 0 ? 0u : S.plane_end[A - 1], g1 = S.plane_end[A];
+    if (g0 == g1) return;
+    const float so = fabsf(comp<B>(r.o)) + fabsf(comp<C>(r.o)), sd = fabsf(comp<B>(r.d)) + fabsf(comp<C>(r.d));
+    for (uint32_t g = g0; g < g1; ++g) {
+        const float4 f0 = S.plane_f[2 * g], f1 = S.plane_f[2 * g + 1];
+        if (live && pair_candidate<A>(r, f0, f1, mlo, mhi, so, sd)) {
+            cand = nc == 0 ? g : nc == 1 ? (cand | g << 8) : cand;
+            ++nc;
+        }
+    }
+}
+
+#if NORI_TU == 0
+__global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
+    __shared__ float4 s_ray[2][kBinBlock];              // (o, mint), (d, maxt)
+    __shared__ float4 s_res[kBinSlots][kBinBlock];      // per (slot, ray): t, u, v, prim | pos << 16
+    __shared__ float4 s_rec[6 * kBinMaxPairs];          // the pairs' records
+    __shared__ uint16_t s_item[kBinBlock / 64][64 * kBinSlots];  // per wave: ray | pair << 8 | slot << 13
+    __shared__ uint32_t s_nitem[kBinBlock / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const SegRange sr = seg_range_k(cnt, G, kTraceSlices / kBinSlices);
+    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % kBinSlices) * kBinBlock, i = i0 + tid;
+    if (i0 >= n) return;  // the whole work-group: its slice is empty
+    const uint32_t np = S.plane_end[2];
+    for (uint32_t j = tid; j < 6 * np; j += kBinBlock) s_rec[j] = S.prims[j];
+    const bool valid = i < n;
+    const uint32_t q = seg_entry(sr, valid ? i : i0);
+    TRay r[1];
+    bool live[1] = {valid};
+    path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
+    scan_prologue<1>(S, r, live);
+    // (1) candidates
+    uint32_t nc = 0, cand = 0;
+    {
+        const float mlo = r[0].mint > 0.0f ? r[0].mint * kPlaneLo : -INF_F;
+        const float mhi = r[0].maxt > 0.0f ? r[0].maxt * kPlaneHi : INF_F;
+        bin_axis<0>(S, r[0], live[0], mlo, mhi, nc, cand);
+        bin_axis<1>(S, r[0], live[0], mlo, mhi, nc, cand);
+        bin_axis<2>(S, r[0], live[0], mlo, mhi, nc, cand);
+    }
+    const bool dense = nc > (uint32_t)kBinSlots;
+    const uint32_t m = dense ? 0u : nc;
+    s_ray[0][tid] = make_float4(r[0].o.x, r[0].o.y, r[0].o.z, r[0].mint);
+    s_ray[1][tid] = make_float4(r[0].d.x, r[0].d.y, r[0].d.z, r[0].maxt);
+    {
+        const uint64_t b1 = __ballot(m >= 1u), b2 = __ballot(m >= 2u);
+        const uint32_t at = rank_in(b1) + rank_in(b2);
+        if (m >= 1u) s_item[w][at] = (uint16_t)(tid | (cand & 31u) << 8);
+        if (m >= 2u) s_item[w][at + 1] = (uint16_t)(tid | ((cand >> 8) & 31u) << 8 | 1u << 13);
+        if (lane == 0) s_nitem[w] = (uint32_t)(__popcll(b1) + __popcll(b2));
+    }
+    // the ray's own tests: every pair for a dense ray, then the other
+    // triangles and the spheres (scan_core's loops)
+    float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
+    uint32_t pb[1] = {0xFFFFFFFFu}, lb[1] = {0u};
+    bool found[1] = {false};
+    if (__any(dense)) {
+        bool dl[1] = {dense && live[0]};
+        scan_planes<0, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
+        scan_planes<1, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
+        scan_planes<2, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
+    }
+    {
+        const uint32_t nt = S.num_scan_tris, nall = S.num_prims;
+        for (uint32_t k = 2 * np; k < nt; k += kScanGroup) {
+            const float4 *p = S.prims + 3 * (size_t)k;
+            float4 qq[3 * kScanGroup];
+#pragma unroll
+            for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
+#pragma unroll
+            for (uint32_t g = 0; g < kScanGroup; ++g)
+                scan_tri<1, false>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
+        }
+        for (uint32_t k = nt; k < nall; ++k) {
+            const float4 *p = S.prims + 3 * (size_t)k;
+            const float4 p0 = p[0], p1 = p[1];
+            const uint32_t pos = __float_as_uint(p[2].w);
+            float t = 0;
+            const bool h = sphere_hit_nb(p0, p1, r[0], t);  // t <= r.maxt = tb
+            if (h && live[0] && (t != tb[0] || pos > lb[0])) {
+                r[0].maxt = tb[0] = t;
+                ub[0] = vb[0] = 0.0f;
+                pb[0] = __float_as_uint(p0.w);
+                lb[0] = pos;
+            }
+        }
+    }
+    __syncthreads();
+    // (2) the work-group's candidates, 64 per wave and round
+    {
+        const uint32_t c0 = s_nitem[0], c1 = c0 + s_nitem[1], c2 = c1 + s_nitem[2], total = c2 + s_nitem[3];
+        for (uint32_t j = w * 64u + lane; j - lane < total; j += kBinBlock) {
+            if (j >= total) continue;
+            const uint32_t k = (j >= c0) + (j >= c1) + (j >= c2);
+            const uint32_t base = k == 0 ? 0u : k == 1 ? c0 : k == 2 ? c1 : c2;
+            const uint32_t item = s_item[k][j - base];
+            const uint32_t rid = item & 255u, g = (item >> 8) & 31u, slot = item >> 13;
+            const float4 ro = s_ray[0][rid], rd = s_ray[1][rid];
+            TRay x;
+            x.o = ld3(ro);
+            x.mint = ro.w;
+            x.d = ld3(rd);
+            x.maxt = rd.w;
+            const float4 *p = s_rec + 6 * g;
+            float4 res = make_float4(INF_F, 0.0f, 0.0f, 0.0f);
+            uint32_t lpos = 0u;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float4 a = p[3 * e], b = p[3 * e + 1], c = p[3 * e + 2];
+                float t = 0, u = 0, v = 0;
+                const uint32_t pos = __float_as_uint(c.w);
+                if (tri_hit_nb(a, b, c, x, t, u, v) && (t != res.x || pos > lpos)) {
+                    res = make_float4(t, u, v, __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | pos << 16));
+                    x.maxt = t;
+                    lpos = pos;
+                }
+            }
+            s_res[slot][rid] = res;
+        }
+    }
+    __syncthreads();
+    // (3) merge
+#pragma unroll
+    for (int s = 0; s < kBinSlots; ++s) {
+        if ((uint32_t)s < m) {
+            const float4 res = s_res[s][tid];
+            const uint32_t wd = __float_as_uint(res.w), pos = wd >> 16;
+            if (res.x < tb[0] || (res.x == tb[0] && pos > lb[0])) {
+                tb[0] = res.x;
+                ub[0] = res.y;
+                vb[0] = res.z;
+                pb[0] = wd & 0xFFFFu;
+                lb[0] = pos;
+            }
+        }
+    }
+    if (valid) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
+}
+
+// NORI_EXTEND_CHECK (diagnostic): mismatching hit records between the two
+// extension kernels on the same queue (t and prim bitwise, u and v as values).
+__device__ unsigned long long g_extend_check[2];
+__global__ __launch_bounds__(kTraceBlock) void k_extend_cmp(const float4 *a, const float4 *b, const uint32_t *cnt,
+                                                            uint32_t G) {
+    const uint32_t e = blockIdx.x * kTraceBlock + threadIdx.x, s = e / kSeg;
+    if (s >= G || e % kSeg >= cnt[s]) return;
+    const float4 x = a[e], y = b[e];
+    const bool same = __float_as_uint(x.x) == __float_as_uint(y.x) && __float_as_uint(x.y) == __float_as_uint(y.y) &&
+                      x.z == y.z && x.w == y.w;
+    atomicAdd(&g_extend_check[1], 1ull);
+    if (!same) atomicAdd(&g_extend_check[0], 1ull);
+}
+#endif
 
 // ------------------------------------------------------------------ shading helpers
 struct SurfHit {
@@ -2585,7 +2794,27 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
+        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
+        const int mode = extend_mode();
+        if (mode == 1 && S.plane_f && S.plane_end[2] <= kBinMaxPairs) {
+            hipLaunchKernelGGL(k_extend_bin, gb, bb, 0, st, S, q, cnt, G);
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
+        if (mode == 2 && S.plane_f && S.plane_end[2] <= kBinMaxPairs) {  // NORI_EXTEND_CHECK
+            static float4 *scratch = nullptr;
+            static size_t have = 0;
+            const size_t need = (size_t)G * kSeg;
+            if (have < need) {
+                if (scratch) (void)hipFree(scratch);
+                if (hipMalloc(&scratch, need * sizeof(float4)) != hipSuccess) return hipErrorOutOfMemory;
+                have = need;
+            }
+            PathQueue q2 = q;
+            q2.hit = scratch;
+            hipLaunchKernelGGL(k_extend_bin, gb, bb, 0, st, S, q2, cnt, G);
+            hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)(need / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
+        }
         return hipGetLastError();
     }
     switch (stack) {
@@ -2709,6 +2938,26 @@ hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Cou
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+// The scan-mode extension kernel: 1 k_extend_bin (default), 0 k_extend_scan
+// (NORI_EXTEND_BIN=0), 2 both on every launch, compared (NORI_EXTEND_CHECK=1).
+int extend_mode() {
+    static const int mode = [] {
+        const char *c = std::getenv("NORI_EXTEND_CHECK");
+        if (c && c[0] == '1') return 2;
+        const char *e = std::getenv("NORI_EXTEND_BIN");
+        if (e) return e[0] == '0' ? 0 : 1;
+        return NORI_EXTEND_BIN ? 1 : 0;
+    }();
+    return mode;
+}
+// NORI_EXTEND_CHECK: read (and reset) the mismatch and compared-entry counts.
+bool extend_check_take(unsigned long long out[2]) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_extend_check), 2 * sizeof(unsigned long long)) != hipSuccess)
+        return false;
+    unsigned long long z[2] = {0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_extend_check), z, sizeof(z)) == hipSuccess;
 }
 
 // NORI_TRAV_STATS builds: read (and reset) the BVH walk counters; false otherwise.

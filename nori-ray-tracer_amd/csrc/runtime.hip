@@ -193,7 +193,7 @@ struct nori_gpu_ctx {
     hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
     nori_camera_desc cam{};
-    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, plane_c;
+    DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, plane_c, plane_f;
     DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
     uint32_t spp = 1;    // the scene's sampleCount (default pass count)
     int stack = 8;       // traversal of extend/shadow: 0 = wave-uniform scan, else LDS stack depth
@@ -388,9 +388,86 @@ bool debug_log();
 struct ScanList {
     std::vector<float> prims;   // 12 floats per record
     std::vector<float> plane_c; // per pair: the plane coordinate c
+    std::vector<float> plane_f; // per pair: the in-plane filter of k_extend_bin (8 floats, plane_filters)
     uint32_t plane_end[3] = {0, 0, 0};  // pairs with axis <= a
     uint32_t tris = 0;          // triangle records (pairs + the rest, padded)
 };
+
+// The in-plane filter of the binned extension kernel (kernels.hip
+// pair_candidate): a ray can be accepted by the Moller-Trumbore test of a
+// triangle of pair g only if its crossing with the pair's plane x_A = c lies
+// within the pair's in-plane bounding rectangle widened by a margin M that
+// covers every rounding error of the test.  Derivation (A the plane axis, B
+// and C the other two, u = 2^-24, gamma_k = k u / (1 - k u)): with e1_A =
+// e2_A = 0, the reference's u numerator tvec . (d x e2) divided by the exact
+// det = -d_A n (n = e1_B e2_C - e1_C e2_B) is a sum of terms bounded by
+// E (|o_B - v0_B| + |o_C - v0_C| + |t*| (|d_B| + |d_C|)) / |n| = E L / |n|
+// (E the largest in-plane edge component, t* = (c - o_A) / d_A the exact
+// crossing), each computed with at most 6 roundings, and det carries
+// (2 kappa + 1) u (kappa <= 32, axis_plane); so the computed u and v differ
+// from the exact barycentrics of the crossing by at most
+// gamma_8 E L / |n| + gamma_(2 kappa + 6) each.  An accepted (u, v) lies in
+// the triangle (u + v <= 1 up to one rounding), hence the exact crossing lies
+// within 2 E (gamma_8 E L / |n| + gamma_(2 kappa + 6)) + 2^-23 E of the
+// triangle's bounding box in B and C.  The kernel computes the crossing as
+// t_f = (c - o_A) * (1 / d_A) (3 roundings of t*) and d_B = o_B + t_f d_B -
+// mid_B, whose own error is below gamma_8 S + 2^-22 |mid_B| with
+// S = |o_B| + |o_C| + |t_f| (|d_B| + |d_C|) >= L - V, V = |v0_B| + |v0_C|.
+// Hence the test  |d_B| <= half_B + Ka S + Kb  (and the same in C) with
+//     Ka = (2 gamma_8 E^2 / n_min + gamma_8) * 1.05
+//     Kb = (2 gamma_8 E^2 / n_min * V + 2 E gamma_70 + 2^-23 E + 2^-22 |mid|) * 1.05
+// never rejects an accepted ray (the factor 1.05 covers the roundings of the
+// filter's own products).  Per pair: (mid_B, half_B + Kb, mid_C, half_C + Kb),
+// (Ka, c, 0, 0).  A padding record (zero edges) never hits and is left out.
+void plane_filters(ScanList &L) {
+    const uint32_t npairs = (uint32_t)L.plane_c.size();
+    L.plane_f.assign(8 * (size_t)npairs, 0.0f);
+    const double u = std::ldexp(1.0, -24);
+    auto gam = [&](double k) { return k * u / (1.0 - k * u); };
+    auto up = [](double x) {  // the float >= x
+        float f = (float)x;
+        return (double)f < x ? std::nextafter(f, INFINITY) : f;
+    };
+    for (uint32_t g = 0; g < npairs; ++g) {
+        const int A = g < L.plane_end[0] ? 0 : g < L.plane_end[1] ? 1 : 2, B = (A + 1) % 3, C = (A + 2) % 3;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double E = 0.0, nmin = INFINITY, V = 0.0;
+        for (int k = 0; k < 2; ++k) {
+            const float *r = &L.prims[12 * (size_t)(2 * g + k)];
+            const float *v0 = r, *e1 = r + 4, *e2 = r + 8;
+            const double n = std::fabs((double)e1[B] * e2[C] - (double)e1[C] * e2[B]);
+            if (n == 0.0) continue;  // padding record
+            for (int a : {B, C}) {
+                for (double x : {(double)v0[a], (double)v0[a] + e1[a], (double)v0[a] + e2[a]}) {
+                    lo[a] = std::min(lo[a], x);
+                    hi[a] = std::max(hi[a], x);
+                }
+                E = std::max({E, std::fabs((double)e1[a]), std::fabs((double)e2[a])});
+            }
+            nmin = std::min(nmin, n);
+            V = std::max(V, std::fabs((double)v0[B]) + std::fabs((double)v0[C]));
+        }
+        float *f = &L.plane_f[8 * (size_t)g];
+        if (!(nmin < INFINITY)) {  // two padding records: an empty rectangle no ray passes
+            f[0] = f[2] = 0.0f;
+            f[1] = f[3] = -1.0f;
+            f[5] = L.plane_c[g];
+            continue;
+        }
+        const double K1 = 2.0 * gam(8) * E * E / nmin;
+        const double Ka = (K1 + gam(8)) * 1.05;
+        for (int k = 0; k < 2; ++k) {
+            const int a = k ? C : B;
+            const float mid = (float)(0.5 * (lo[a] + hi[a]));
+            const double half = std::max(hi[a] - mid, mid - lo[a]);
+            const double Kb = (K1 * V + 2.0 * E * gam(70) + std::ldexp(E, -23) + std::ldexp(std::fabs(mid), -22)) * 1.05;
+            f[2 * k] = mid;
+            f[2 * k + 1] = (float)up(up(half) + Kb);
+        }
+        f[4] = (float)up(Ka);
+        f[5] = L.plane_c[g];
+    }
+}
 bool axis_plane(const float *r, int a) {
     const float *e1 = r + 4, *e2 = r + 8;
     if (e1[a] != 0.0f || e2[a] != 0.0f) return false;
@@ -460,6 +537,7 @@ ScanList build_scan_list(const DeviceBvh &bvh, uint32_t n) {
     L.tris += rest;
     for (uint32_t i = 0; i < n; ++i)
         if (sphere(i)) add(i);
+    plane_filters(L);
     if (const char *e = std::getenv("NORI_PLANE_CULL"); e && e[0] == '0') {  // A/B: no plane pairs
         ScanList F;
         for (uint32_t i = 0; i < n; ++i)
@@ -736,6 +814,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     c.nodes.upload(bvh.nodes);
     c.prims.upload(prim_list);
     if (!scan_list.plane_c.empty()) c.plane_c.upload(scan_list.plane_c);
+    if (!scan_list.plane_f.empty()) c.plane_f.upload(scan_list.plane_f);
     c.tri_vidx.upload(tri_vidx);
     c.pos.upload(pos);
     c.nrm.upload(nrm);
@@ -787,6 +866,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.num_prims = (uint32_t)(prim_list.size() / 12);
     S.num_scan_tris = scan_list.tris;
     S.plane_c = scan_list.plane_c.empty() ? nullptr : c.plane_c.as<float>();
+    S.plane_f = scan_list.plane_f.empty() ? nullptr : c.plane_f.as<float4>();
     for (int a = 0; a < 3; ++a) S.plane_end[a] = scan_list.plane_end[a];
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     S.blob = use_blob ? c.blob.as<float4>() : nullptr;
@@ -1360,6 +1440,13 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             finish_rays += st.w;
         }
         invalid += hc.invalid;
+        if (c.stack == 0 && extend_mode() == 2) {  // NORI_EXTEND_CHECK: the two extension kernels must agree
+            unsigned long long ck[2] = {0, 0};
+            if (extend_check_take(ck) && (debug_log() || ck[0]))
+                std::fprintf(stderr, "[nori] extension check: %llu of %llu hit records differ\n", ck[0], ck[1]);
+            if (ck[0]) throw NoriException(NORI_ERR_INVALID, "extension check: k_extend_bin and k_extend_scan differ on " +
+                                                              std::to_string(ck[0]) + " of " + std::to_string(ck[1]) + " rays");
+        }
         if (debug_log())
         {
             unsigned long long ts[8];
@@ -1497,16 +1584,18 @@ double share_samples(int W, int H, const nori_gpu_render_desc &s) {
 // communicator.  Only a peer that cannot join at all (its device faulted,
 // its process died) is waited for: every other failure reaches the peers
 // through the status exchange.  NORI_COMM_TIMEOUT_S fixes the bound;
-// otherwise it scales with the frame: max(30 s, 20 x this rank's own render
-// time x largest share / own share), since every peer renders a share of
-// about the same size with the same code.  A rank without a share has no time
-// of its own and waits up to 600 s.
-double comm_timeout_s(double own_s, double own_samples, double max_samples) {
+// otherwise, for a rank that rendered its share (status NORI_OK), it scales
+// with the frame: max(30 s, 20 x this rank's own render time x largest share
+// / own share), since every peer renders a share of about the same size with
+// the same code.  A rank whose own render failed or was cancelled, or that
+// has no share, has no render time that says how long its peers need: it
+// waits up to 600 s.
+double comm_timeout_s(int status, double own_s, double own_samples, double max_samples) {
     if (const char *e = std::getenv("NORI_COMM_TIMEOUT_S")) {
         const double v = std::atof(e);
         if (v > 0.0) return v;
     }
-    if (!(own_samples > 0.0)) return 600.0;
+    if (status != NORI_OK || !(own_samples > 0.0)) return 600.0;
     return std::max(30.0, 20.0 * own_s * std::max(1.0, max_samples / own_samples));
 }
 
@@ -1604,6 +1693,29 @@ int nori_scene_bvh_info(const nori_scene_desc *d, nori_bvh_info *out) {
             for (int k = 0; k < 4; ++k) h = (h ^ ((id >> (8 * k)) & 0xFFu)) * 1099511628211ull;
         }
         out->order_hash = h;
+        return NORI_OK;
+    });
+}
+int nori_scene_scan_list(const nori_scene_desc *d, nori_scan_info *info, float *records, float *plane_c,
+                         float *plane_f) {
+    return guarded([&] {
+        if (!d || !info) return fail(NORI_ERR_INVALID, "null argument");
+        if (d->abi_version != NORI_GPU_ABI_VERSION) return fail(NORI_ERR_INVALID, "ABI version mismatch");
+        float rmin[3], rmax[3];
+        scene_root_box(*d, rmin, rmax);
+        DeviceBvh bvh;
+        build_device_bvh(*d, rmin, rmax, bvh);
+        const uint32_t n = (uint32_t)(bvh.prims.size() / 12);
+        std::memset(info, 0, sizeof(*info));
+        if (n > kScanMaxPrims) return NORI_OK;  // a BVH scene: no scan list
+        const ScanList L = build_scan_list(bvh, n);
+        info->records = (uint32_t)(L.prims.size() / 12);
+        info->pairs = (uint32_t)L.plane_c.size();
+        for (int a = 0; a < 3; ++a) info->plane_end[a] = L.plane_end[a];
+        info->tris = L.tris;
+        if (records) std::memcpy(records, L.prims.data(), L.prims.size() * 4);
+        if (plane_c && !L.plane_c.empty()) std::memcpy(plane_c, L.plane_c.data(), L.plane_c.size() * 4);
+        if (plane_f && !L.plane_f.empty()) std::memcpy(plane_f, L.plane_f.data(), L.plane_f.size() * 4);
         return NORI_OK;
     });
 }
@@ -1809,7 +1921,7 @@ int nori_gpu_render_sharded(nori_gpu_ctx *c, nori_gpu_comm *comm, const nori_gpu
                 return fail(rc, err);
             }
         }
-        const double timeout = comm_timeout_s(own_s, own_samples, max_samples);
+        const double timeout = comm_timeout_s(rc, own_s, own_samples, max_samples);
         const int all = comm_max_int(comm->nccl, comm->status_dev, comm->status_host,
                                      comm_status_word(rc, comm->rank), c->stream, timeout, comm->aborted);
         if (rc != NORI_OK) return fail(rc, err);
@@ -1823,8 +1935,8 @@ int nori_gpu_render_sharded(nori_gpu_ctx *c, nori_gpu_comm *comm, const nori_gpu
     });
 }
 int nori_gpu_comm_status_word(int rc, int rank) { return comm_status_word(rc, rank); }
-double nori_gpu_comm_timeout(double own_seconds, double own_samples, double max_samples) {
-    return comm_timeout_s(own_seconds, own_samples, max_samples);
+double nori_gpu_comm_timeout(int status, double own_seconds, double own_samples, double max_samples) {
+    return comm_timeout_s(status, own_seconds, own_samples, max_samples);
 }
 void nori_gpu_destroy(nori_gpu_ctx *c) {
     if (!c) return;

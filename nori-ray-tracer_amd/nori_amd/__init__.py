@@ -41,11 +41,13 @@ class Scene:
         self.path = path
         self.desc_ptr = lib().nori_scene_get_desc(self._h)
         self.desc = self.desc_ptr.contents
+        # kept on the instance: at interpreter exit the module globals may be gone before __del__ runs
+        self._free = lib().nori_scene_free
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value and _abi._lib is not None:
-            _abi._lib.nori_scene_free(h)
+        h, free = getattr(self, "_h", None), getattr(self, "_free", None)
+        if h is not None and h.value and free is not None:
+            free(h)
             self._h = None
 
     # convenience views
@@ -204,6 +206,24 @@ def bvh_info(scene):
     return {k: getattr(info, k) for k, _ in BvhInfo._fields_ if k != "pad"}
 
 
+class ScanInfo(C.Structure):
+    _fields_ = [("records", C.c_uint32), ("pairs", C.c_uint32), ("plane_end", C.c_uint32 * 3), ("tris", C.c_uint32)]
+
+
+def scan_list(scene):
+    """The small-scene scan list as the GPU context builds it (nori_scene_scan_list): a dict with
+    records (n, 12) float32, plane_c (pairs,), plane_f (pairs, 8), plane_end (3,), tris; records is
+    empty for a BVH scene."""
+    info = ScanInfo()
+    check(lib().nori_scene_scan_list(scene.desc_ptr, C.byref(info), None, None, None))
+    rec = np.zeros((info.records, 12), np.float32)
+    pc = np.zeros(max(info.pairs, 1), np.float32)
+    pf = np.zeros((max(info.pairs, 1), 8), np.float32)
+    check(lib().nori_scene_scan_list(scene.desc_ptr, C.byref(info), _fptr(rec), _fptr(pc), _fptr(pf)))
+    return {"records": rec, "plane_c": pc[:info.pairs], "plane_f": pf[:info.pairs],
+            "plane_end": np.array(list(info.plane_end)), "tris": info.tris}
+
+
 def read_exr(path):
     """R, G, B planes of an OpenEXR file as a (height, width, 3) float32 array (nori_read_exr)."""
     w, h = C.c_int(), C.c_int()
@@ -232,12 +252,13 @@ class GpuRenderer:
         h = C.c_void_p()
         check(lib().nori_gpu_create(scene.desc_ptr, int(device), C.byref(h)))
         self._h = h
+        self._destroy = lib().nori_gpu_destroy  # usable in __del__ at interpreter exit
         self.device = device
         self.last_stats = None
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
-            lib().nori_gpu_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     def __del__(self):

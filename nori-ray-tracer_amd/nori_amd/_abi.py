@@ -132,6 +132,8 @@ SIGNATURES = {
     "nori_read_exr": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)]),
     "nori_read_image": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint8)]),
     "nori_scene_bvh_info": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "nori_scene_scan_list": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                       C.POINTER(C.c_float)]),
     "nori_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nori_gpu_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "nori_gpu_render": (C.c_int, [C.c_void_p, C.POINTER(RenderDesc), C.c_void_p, C.POINTER(Stats)]),
@@ -149,7 +151,7 @@ SIGNATURES = {
     "nori_gpu_render_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(RenderDesc), C.c_int, C.c_int,
                                           C.c_void_p, C.POINTER(Stats)]),
     "nori_gpu_comm_status_word": (C.c_int, [C.c_int, C.c_int]),
-    "nori_gpu_comm_timeout": (C.c_double, [C.c_double, C.c_double, C.c_double]),
+    "nori_gpu_comm_timeout": (C.c_double, [C.c_int, C.c_double, C.c_double, C.c_double]),
 }
 
 COMM_ID_BYTES = 128

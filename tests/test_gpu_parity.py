@@ -218,7 +218,8 @@ def test_plane_cull_same_hits(built):
     them (NORI_PLANE_CULL=0, read at context creation): the same hit on every
     ray -- t bit for bit -- and the same image up to the film sums' order.
     Rays include grazing ones (direction components of 1e-7 .. 1e-3 towards
-    the walls) and origins on the wall planes."""
+    the walls), origins on the wall planes, and origins on the planes with
+    mint = 0 (a t = 0 hit the culls must keep)."""
     s = nori_amd.load_scene(scene_path("pa4", "cbox", "cbox_path_mis.xml"), 64, 48, 8)
     rays = np.concatenate([_rays(30000, 21, [-0.9, 0.05, -0.9], [0.9, 1.5, 0.9]),
                            _rays(5000, 22, [-3, -1, -3], [3, 3, 6], mint=0.01)])
@@ -233,7 +234,9 @@ def test_plane_cull_same_hits(built):
     on[which == 1, 1] = 1.59
     on[which == 2, 0] = 1.0
     on[which == 3, 2] = -1.04
-    rays = np.concatenate([rays, graze, on]).astype(np.float32)
+    zero = on.copy()  # mint = 0 (trace API): Moller-Trumbore accepts t = +-0 on the plane itself
+    zero[:, 3] = 0.0
+    rays = np.concatenate([rays, graze, on, zero]).astype(np.float32)
     sh = rays.copy()
     sh[:, 7] = np.random.default_rng(23).uniform(0.01, 2.0, size=sh.shape[0])
     os.environ["NORI_PLANE_CULL"] = "0"

@@ -126,15 +126,32 @@ def test_status_word_encoding(built):
 
 
 def test_comm_timeout_scales_with_the_share(built, monkeypatch):
-    """Watchdog bound of the sharded collectives: max(30 s, 20 x own render
-    time x largest share / own share); 600 s without a share; the env wins."""
+    """Watchdog bound of the sharded collectives after a rendered share:
+    max(30 s, 20 x own render time x largest share / own share); 600 s
+    without a share; the env wins."""
     from nori_amd import _abi
     monkeypatch.delenv("NORI_COMM_TIMEOUT_S", raising=False)
     f = _abi.lib().nori_gpu_comm_timeout
-    assert f(0.03, 1e6, 1e6) == 30.0           # a 30 ms frame: the 30 s floor
-    assert f(10.0, 1e6, 1e6) == 200.0          # 20x a 10 s share
-    assert f(10.0, 1e6, 2e6) == 400.0          # a peer holds twice the samples
-    assert f(10.0, 2e6, 1e6) == 200.0          # never below the own share's bound
-    assert f(0.0, 0.0, 1e6) == 600.0           # no share: no own time to scale
+    ok = _abi.NORI_OK
+    assert f(ok, 0.03, 1e6, 1e6) == 30.0           # a 30 ms frame: the 30 s floor
+    assert f(ok, 10.0, 1e6, 1e6) == 200.0          # 20x a 10 s share
+    assert f(ok, 10.0, 1e6, 2e6) == 400.0          # a peer holds twice the samples
+    assert f(ok, 10.0, 2e6, 1e6) == 200.0          # never below the own share's bound
+    assert f(ok, 0.0, 0.0, 1e6) == 600.0           # no share: no own time to scale
     monkeypatch.setenv("NORI_COMM_TIMEOUT_S", "5")
-    assert f(10.0, 1e6, 1e6) == 5.0
+    assert f(ok, 10.0, 1e6, 1e6) == 5.0
+    assert f(_abi.NORI_ERR_CANCELLED, 0.01, 1e6, 1e6) == 5.0
+
+
+def test_comm_timeout_of_a_failed_or_cancelled_rank(built, monkeypatch):
+    """A rank whose own render threw (own time never measured: 0) or was
+    cancelled early (a truncated time) must not fall to the 30 s floor or to
+    a bound scaled from that time: its peers may render for much longer, so it
+    keeps the fixed 600 s bound."""
+    from nori_amd import _abi
+    monkeypatch.delenv("NORI_COMM_TIMEOUT_S", raising=False)
+    f = _abi.lib().nori_gpu_comm_timeout
+    for rc in (_abi.NORI_ERR_CANCELLED, _abi.NORI_ERR_OOM, _abi.NORI_ERR_INVALID, _abi.NORI_ERR_HIP):
+        assert f(rc, 0.0, 1e6, 1e6) == 600.0       # threw before its time was taken
+        assert f(rc, 0.5, 1e6, 1e6) == 600.0       # cancelled after 0.5 s
+        assert f(rc, 100.0, 1e6, 1e6) == 600.0     # never a bound scaled from a failed share

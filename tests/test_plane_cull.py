@@ -38,11 +38,14 @@ def moller_trumbore(p0, e1, e2, o, d, mint, maxt):
 
 
 def may_hit(o, d, c, mint, maxt):
+    """kernels.hip plane_may_hit (no bound on a side where mint <= 0 / maxt <= 0)."""
     with np.errstate(all="ignore"):
         T = o - c
         ad = np.abs(d)
         s = np.where(d > 0, -T, T)
-        return (s > mint * LO * ad) & (s < maxt * HI * ad)
+        lo = np.where(mint > 0, mint * LO * ad, f32(-np.inf)).astype(f32)
+        hi = np.where(maxt > 0, maxt * HI * ad, f32(np.inf)).astype(f32)
+        return (s > lo) & (s < hi)
 
 
 def plane_triangles():
@@ -95,6 +98,24 @@ def test_cull_implies_reject(built):
         culled += int((~may).sum())
         checked += len(o)
     assert culled > checked // 4  # the cull is not vacuous
+
+
+def test_cull_with_zero_mint_keeps_plane_hits(built):
+    """mint = 0 (the trace API passes the caller's mint): origins on the plane
+    are hit at t = +-0, which the cull must not skip."""
+    rng = np.random.default_rng(9)
+    kept = 0
+    for p0, e1, e2, a in plane_triangles():
+        c = p0[a]
+        o, d = rays(rng, 50000)
+        o[:, a] = c
+        mint = np.zeros(len(o), f32)
+        maxt = np.full(len(o), np.inf, f32)
+        hit, t = moller_trumbore(p0, e1, e2, (o[:, 0], o[:, 1], o[:, 2]), (d[:, 0], d[:, 1], d[:, 2]), mint, maxt)
+        may = may_hit(o[:, a], d[:, a], c, mint, maxt)
+        assert not (hit & ~may).any()
+        kept += int((hit & (t == 0)).sum())
+    assert kept > 1000  # t = 0 hits exist and are kept
 
 
 def moller_trumbore_plane(p0, e1, e2, o, d, mint, maxt, A):
