@@ -771,29 +771,35 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
 }
 
 // ------------------------------------------------------------------ binned extension scan
-// k_extend_scan tests every axis-plane pair against every ray; a ray inside
-// the Cornell box can be accepted by one wall (where it leaves the box), so
-// most of those tests are wasted, yet a 64-ray wave always holds some ray for
-// every wall.  k_extend_bin therefore moves the pair tests out of the ray's
-// lane: (1) every lane filters its ray against each pair -- a dozen VALU
-// instructions (pair_candidate, exact: runtime.hip plane_filters) -- and
-// hands the (ray, pair) candidates to a work-group list in LDS, while it
-// scans the remaining triangles and the spheres itself as before; (2) the
-// work-group's four waves run the listed candidates 64 at a time, each lane
-// one (ray, pair) with the pair's two records and the ray read from LDS --
-// dense lanes whatever pair they belong to; (3) every lane merges its
-// candidates' results into its own closest hit.  The tie rule of scan_core
-// (closest t, then the later leaf position) makes the result independent of
-// the order of the tests, so the hits are those of k_extend_scan bit for bit
-// (NORI_EXTEND_CHECK compares the two on every launch).  A ray with more
-// than kBinSlots candidate pairs tests every pair in its own lane.
+// k_extend_scan tests every axis-plane pair and every sphere against every
+// ray; a ray inside the Cornell box can be accepted by one wall (where it
+// leaves the box) and passes near a sphere rarely, so most of those tests are
+// wasted, yet a 64-ray wave always holds some ray for every wall.
+// k_extend_bin therefore moves those tests out of the ray's lane: (1) every
+// lane filters its ray against each pair -- a dozen VALU instructions
+// (pair_candidate, exact: runtime.hip plane_filters) -- and each sphere --
+// the reference's own discriminant, disc > 0 being the sphere test's first
+// condition -- and hands the (ray, pair) and (ray, sphere) candidates to two
+// work-group lists in LDS, while it scans the remaining triangles itself as
+// before; (2) the work-group's four waves run the listed candidates 64 at a
+// time, pairs first, then spheres, each lane one candidate with the records
+// and the ray read from LDS -- dense lanes whatever ray they belong to; (3)
+// every lane merges its candidates' results into its own closest hit.  The
+// tie rule of scan_core (closest t, then the later leaf position) makes the
+// result independent of the order of the tests, so the hits are those of
+// k_extend_scan bit for bit (NORI_EXTEND_CHECK compares the two on every
+// launch).  A ray with more than kBinSlots candidates tests everything in its
+// own lane.
 #ifndef NORI_EXTEND_BIN
 #define NORI_EXTEND_BIN 1
 #endif
+#ifndef NORI_BIN_SPHERES
+#define NORI_BIN_SPHERES 1
+#endif
 constexpr int kBinBlock = 256;
 constexpr uint32_t kBinSlices = kTraceGroup * kSeg / kBinBlock;  // work-groups per group of segments
-constexpr int kBinSlots = 2;
-constexpr uint32_t kBinMaxPairs = 32;
+constexpr int kBinSlots = 3;
+constexpr uint32_t kBinMaxRec = 64;  // staged records: the pairs' (2 per pair) and the spheres'
 template <int A>
 ND float comp(const V3 &v) { return A == 0 ? v.x : A == 1 ? v.y : v.z; }
 
@@ -814,36 +820,53 @@ ND bool pair_candidate(const TRay &r, const float4 &f0, const float4 &f1, float 
     return tf > mlo && tf <= mhi && !(fabsf(dB) > thB) && !(fabsf(dC) > thC);
 }
 
-// This ray's candidate pairs of axis A: the count and the first kBinSlots
-// pair indices (5 bits each, 8 bits apart).
+// A ray's candidates: count and up to kBinSlots entries of 8 bits (kind << 7
+// | index: kind 0 a pair, 1 a sphere), 8 bits apart.
+struct BinCand {
+    uint32_t n = 0, e = 0;
+    ND void add(uint32_t v) {
+        e = n < (uint32_t)kBinSlots ? (e | v << (8 * n)) : e;
+        ++n;
+    }
+};
 template <int A>
-ND void bin_axis(const DevScene &S, const TRay &r, bool live, float mlo, float mhi, uint32_t &nc, uint32_t &cand) {
+ND void bin_axis(const DevScene &S, const TRay &r, bool live, float mlo, float mhi, BinCand &bc) {
     constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
     const uint32_t g0 = A == 0 ? 0u : S.plane_end[A - 1], g1 = S.plane_end[A];
     if (g0 == g1) return;
     const float so = fabsf(comp<B>(r.o)) + fabsf(comp<C>(r.o)), sd = fabsf(comp<B>(r.d)) + fabsf(comp<C>(r.d));
     for (uint32_t g = g0; g < g1; ++g) {
         const float4 f0 = S.plane_f[2 * g], f1 = S.plane_f[2 * g + 1];
-        if (live && pair_candidate<A>(r, f0, f1, mlo, mhi, so, sd)) {
-            cand = nc == 0 ? g : nc == 1 ? (cand | g << 8) : cand;
-            ++nc;
-        }
+        if (live && pair_candidate<A>(r, f0, f1, mlo, mhi, so, sd)) bc.add(g);
     }
+}
+// The discriminant of Sphere::rayIntersect (sphere.cpp:43-76) exactly as
+// sphere_hit_nb computes it: disc > 0 is the test's first condition.
+ND float sphere_disc(const float4 &a, const float4 &b, const TRay &r) {
+    V3 oc = r.o - ld3(a);
+    float rad = b.x;
+    float A = dot(r.d, r.d);
+    float B = 2.0f * dot(oc, r.d);
+    float C = dot(oc, oc) - rad * rad;
+    return B * B - 4 * A * C;
 }
 
 #if NORI_TU == 0
 __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
+    constexpr uint32_t NW = kBinBlock / 64, CAP = 64 * kBinSlots;
     __shared__ float4 s_ray[2][kBinBlock];              // (o, mint), (d, maxt)
     __shared__ float4 s_res[kBinSlots][kBinBlock];      // per (slot, ray): t, u, v, prim | pos << 16
-    __shared__ float4 s_rec[6 * kBinMaxPairs];          // the pairs' records
-    __shared__ uint16_t s_item[kBinBlock / 64][64 * kBinSlots];  // per wave: ray | pair << 8 | slot << 13
-    __shared__ uint32_t s_nitem[kBinBlock / 64];
+    __shared__ float4 s_rec[3 * kBinMaxRec];            // the pairs' records, then the spheres'
+    __shared__ uint16_t s_item[2][NW][CAP];             // per kind and wave: ray | index << 8 | slot << 14
+    __shared__ uint32_t s_nitem[2][NW];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const SegRange sr = seg_range_k(cnt, G, kTraceSlices / kBinSlices);
     const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % kBinSlices) * kBinBlock, i = i0 + tid;
     if (i0 >= n) return;  // the whole work-group: its slice is empty
-    const uint32_t np = S.plane_end[2];
+    const uint32_t np = S.plane_end[2], nt = S.num_scan_tris, nall = S.num_prims;
+    const uint32_t ns = NORI_BIN_SPHERES ? nall - nt : 0u, sph0 = 6 * np;
     for (uint32_t j = tid; j < 6 * np; j += kBinBlock) s_rec[j] = S.prims[j];
+    for (uint32_t j = tid; j < 3 * ns; j += kBinBlock) s_rec[sph0 + j] = S.prims[3 * nt + j];
     const bool valid = i < n;
     const uint32_t q = seg_entry(sr, valid ? i : i0);
     TRay r[1];
@@ -851,90 +874,121 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
     path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
     scan_prologue<1>(S, r, live);
     // (1) candidates
-    uint32_t nc = 0, cand = 0;
+    BinCand bc;
     {
         const float mlo = r[0].mint > 0.0f ? r[0].mint * kPlaneLo : -INF_F;
         const float mhi = r[0].maxt > 0.0f ? r[0].maxt * kPlaneHi : INF_F;
-        bin_axis<0>(S, r[0], live[0], mlo, mhi, nc, cand);
-        bin_axis<1>(S, r[0], live[0], mlo, mhi, nc, cand);
-        bin_axis<2>(S, r[0], live[0], mlo, mhi, nc, cand);
+        bin_axis<0>(S, r[0], live[0], mlo, mhi, bc);
+        bin_axis<1>(S, r[0], live[0], mlo, mhi, bc);
+        bin_axis<2>(S, r[0], live[0], mlo, mhi, bc);
     }
-    const bool dense = nc > (uint32_t)kBinSlots;
-    const uint32_t m = dense ? 0u : nc;
+    for (uint32_t k = 0; k < ns; ++k) {
+        const float4 *p = S.prims + 3 * (size_t)(nt + k);
+        if (live[0] && sphere_disc(p[0], p[1], r[0]) > 0.0f) bc.add(128u | k);
+    }
+    const bool dense = bc.n > (uint32_t)kBinSlots;
+    const uint32_t m = dense ? 0u : bc.n;
     s_ray[0][tid] = make_float4(r[0].o.x, r[0].o.y, r[0].o.z, r[0].mint);
     s_ray[1][tid] = make_float4(r[0].d.x, r[0].d.y, r[0].d.z, r[0].maxt);
-    {
-        const uint64_t b1 = __ballot(m >= 1u), b2 = __ballot(m >= 2u);
-        const uint32_t at = rank_in(b1) + rank_in(b2);
-        if (m >= 1u) s_item[w][at] = (uint16_t)(tid | (cand & 31u) << 8);
-        if (m >= 2u) s_item[w][at + 1] = (uint16_t)(tid | ((cand >> 8) & 31u) << 8 | 1u << 13);
-        if (lane == 0) s_nitem[w] = (uint32_t)(__popcll(b1) + __popcll(b2));
+#pragma unroll
+    for (uint32_t kind = 0; kind < 2; ++kind) {
+        uint32_t mk = 0;
+#pragma unroll
+        for (int e = 0; e < kBinSlots; ++e) mk += ((uint32_t)e < m && ((bc.e >> (8 * e + 7)) & 1u) == kind) ? 1u : 0u;
+        const uint64_t b1 = __ballot(mk >= 1u), b2 = __ballot(mk >= 2u), b3 = __ballot(mk >= 3u);
+        uint32_t at = rank_in(b1) + rank_in(b2) + rank_in(b3);
+#pragma unroll
+        for (int e = 0; e < kBinSlots; ++e) {
+            const uint32_t v = (bc.e >> (8 * e)) & 255u;
+            if ((uint32_t)e < m && (v >> 7) == kind) s_item[kind][w][at++] = (uint16_t)(tid | (v & 63u) << 8 | (uint32_t)e << 14);
+        }
+        if (lane == 0) s_nitem[kind][w] = (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
     }
-    // the ray's own tests: every pair for a dense ray, then the other
-    // triangles and the spheres (scan_core's loops)
+    // the ray's own tests: every pair and sphere for a dense ray, then the
+    // other triangles (scan_core's loops)
     float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
     uint32_t pb[1] = {0xFFFFFFFFu}, lb[1] = {0u};
     bool found[1] = {false};
+    auto sphere_own = [&](uint32_t k, bool on) {
+        const float4 *p = S.prims + 3 * (size_t)k;
+        const float4 p0 = p[0], p1 = p[1];
+        const uint32_t pos = __float_as_uint(p[2].w);
+        float t = 0;
+        const bool h = sphere_hit_nb(p0, p1, r[0], t);  // t <= r.maxt = tb
+        if (h && on && (t != tb[0] || pos > lb[0])) {
+            r[0].maxt = tb[0] = t;
+            ub[0] = vb[0] = 0.0f;
+            pb[0] = __float_as_uint(p0.w);
+            lb[0] = pos;
+        }
+    };
     if (__any(dense)) {
         bool dl[1] = {dense && live[0]};
         scan_planes<0, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
         scan_planes<1, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
         scan_planes<2, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
+        for (uint32_t k = nt; k < nt + ns; ++k) sphere_own(k, dl[0]);
     }
-    {
-        const uint32_t nt = S.num_scan_tris, nall = S.num_prims;
-        for (uint32_t k = 2 * np; k < nt; k += kScanGroup) {
-            const float4 *p = S.prims + 3 * (size_t)k;
-            float4 qq[3 * kScanGroup];
+    for (uint32_t k = 2 * np; k < nt; k += kScanGroup) {
+        const float4 *p = S.prims + 3 * (size_t)k;
+        float4 qq[3 * kScanGroup];
 #pragma unroll
-            for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
+        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
 #pragma unroll
-            for (uint32_t g = 0; g < kScanGroup; ++g)
-                scan_tri<1, false>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
-        }
-        for (uint32_t k = nt; k < nall; ++k) {
-            const float4 *p = S.prims + 3 * (size_t)k;
-            const float4 p0 = p[0], p1 = p[1];
-            const uint32_t pos = __float_as_uint(p[2].w);
-            float t = 0;
-            const bool h = sphere_hit_nb(p0, p1, r[0], t);  // t <= r.maxt = tb
-            if (h && live[0] && (t != tb[0] || pos > lb[0])) {
-                r[0].maxt = tb[0] = t;
-                ub[0] = vb[0] = 0.0f;
-                pb[0] = __float_as_uint(p0.w);
-                lb[0] = pos;
-            }
-        }
+        for (uint32_t g = 0; g < kScanGroup; ++g)
+            scan_tri<1, false>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
+    for (uint32_t k = nt + ns; k < nall; ++k) sphere_own(k, live[0]);  // (NORI_BIN_SPHERES=0)
     __syncthreads();
-    // (2) the work-group's candidates, 64 per wave and round
+    // (2) the work-group's candidates, 64 per wave and round: pairs, then spheres
     {
-        const uint32_t c0 = s_nitem[0], c1 = c0 + s_nitem[1], c2 = c1 + s_nitem[2], total = c2 + s_nitem[3];
-        for (uint32_t j = w * 64u + lane; j - lane < total; j += kBinBlock) {
-            if (j >= total) continue;
-            const uint32_t k = (j >= c0) + (j >= c1) + (j >= c2);
-            const uint32_t base = k == 0 ? 0u : k == 1 ? c0 : k == 2 ? c1 : c2;
-            const uint32_t item = s_item[k][j - base];
-            const uint32_t rid = item & 255u, g = (item >> 8) & 31u, slot = item >> 13;
+        uint32_t pre[2][NW + 1];
+#pragma unroll
+        for (int kind = 0; kind < 2; ++kind) {
+            pre[kind][0] = 0;
+#pragma unroll
+            for (uint32_t v = 0; v < NW; ++v) pre[kind][v + 1] = pre[kind][v] + s_nitem[kind][v];
+        }
+        const uint32_t nc0 = (pre[0][NW] + 63u) / 64u, nch = nc0 + (pre[1][NW] + 63u) / 64u;
+        for (uint32_t c = w; c < nch; c += NW) {
+            const uint32_t kind = c < nc0 ? 0u : 1u, j = (kind ? c - nc0 : c) * 64u + lane;
+            if (j >= pre[kind][NW]) continue;
+            uint32_t k = 0;
+#pragma unroll
+            for (uint32_t v = 1; v < NW; ++v) k += j >= pre[kind][v] ? 1u : 0u;
+            uint32_t base = 0;
+#pragma unroll
+            for (uint32_t v = 1; v < NW; ++v) base = k == v ? pre[kind][v] : base;
+            const uint32_t item = s_item[kind][k][j - base];
+            const uint32_t rid = item & 255u, idx = (item >> 8) & 63u, slot = item >> 14;
             const float4 ro = s_ray[0][rid], rd = s_ray[1][rid];
             TRay x;
             x.o = ld3(ro);
             x.mint = ro.w;
             x.d = ld3(rd);
             x.maxt = rd.w;
-            const float4 *p = s_rec + 6 * g;
             float4 res = make_float4(INF_F, 0.0f, 0.0f, 0.0f);
-            uint32_t lpos = 0u;
+            if (kind == 0) {
+                const float4 *p = s_rec + 6 * idx;
+                uint32_t lpos = 0u;
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const float4 a = p[3 * e], b = p[3 * e + 1], c = p[3 * e + 2];
-                float t = 0, u = 0, v = 0;
-                const uint32_t pos = __float_as_uint(c.w);
-                if (tri_hit_nb(a, b, c, x, t, u, v) && (t != res.x || pos > lpos)) {
-                    res = make_float4(t, u, v, __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | pos << 16));
-                    x.maxt = t;
-                    lpos = pos;
+                for (int e = 0; e < 2; ++e) {
+                    const float4 a = p[3 * e], b = p[3 * e + 1], c = p[3 * e + 2];
+                    float t = 0, u = 0, v = 0;
+                    const uint32_t pos = __float_as_uint(c.w);
+                    if (tri_hit_nb(a, b, c, x, t, u, v) && (t != res.x || pos > lpos)) {
+                        res = make_float4(t, u, v, __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | pos << 16));
+                        x.maxt = t;
+                        lpos = pos;
+                    }
                 }
+            } else {
+                const float4 *p = s_rec + sph0 + 3 * idx;
+                const float4 a = p[0];
+                float t = 0;
+                if (sphere_hit_nb(a, p[1], x, t))
+                    res = make_float4(t, 0.0f, 0.0f,
+                                      __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | __float_as_uint(p[2].w) << 16));
             }
             s_res[slot][rid] = res;
         }
@@ -942,9 +996,9 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
     __syncthreads();
     // (3) merge
 #pragma unroll
-    for (int s = 0; s < kBinSlots; ++s) {
-        if ((uint32_t)s < m) {
-            const float4 res = s_res[s][tid];
+    for (int e = 0; e < kBinSlots; ++e) {
+        if ((uint32_t)e < m) {
+            const float4 res = s_res[e][tid];
             const uint32_t wd = __float_as_uint(res.w), pos = wd >> 16;
             if (res.x < tb[0] || (res.x == tb[0] && pos > lb[0])) {
                 tb[0] = res.x;
@@ -2796,12 +2850,13 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
         const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
         const int mode = extend_mode();
-        if (mode == 1 && S.plane_f && S.plane_end[2] <= kBinMaxPairs) {
+        const bool bin_ok = S.plane_f && 2 * S.plane_end[2] + (S.num_prims - S.num_scan_tris) <= kBinMaxRec;
+        if (mode == 1 && bin_ok) {
             hipLaunchKernelGGL(k_extend_bin, gb, bb, 0, st, S, q, cnt, G);
             return hipGetLastError();
         }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
-        if (mode == 2 && S.plane_f && S.plane_end[2] <= kBinMaxPairs) {  // NORI_EXTEND_CHECK
+        if (mode == 2 && bin_ok) {  // NORI_EXTEND_CHECK
             static float4 *scratch = nullptr;
             static size_t have = 0;
             const size_t need = (size_t)G * kSeg;
