@@ -163,7 +163,8 @@ def roofline(ts, samples, config="c2"):
         if prof:
             row["traffic_bytes_per_launch"] = prof.get("hbm_bytes_per_launch")
             row["rocprof_avg_launch_ms"] = prof.get("trace_avg_ms")
-            # the counters come from the committed profile, collected at this commit
+            # the counters come from the committed profile, collected at the commit recorded in it
+            # ("commit"): when the kernel sources changed after that commit they describe the older kernel
             row["profile"] = {"file": prof["file"], "commit": prof.get("commit"), "kernel": prof["name"]}
             if prof.get("sq_insts_valu_per_launch") and prof.get("trace_avg_ms"):
                 rate = prof["sq_insts_valu_per_launch"] * 64 / (prof["trace_avg_ms"] / 1e3)

@@ -389,7 +389,8 @@ static __device__ unsigned long long g_trav_stats[8];
 // LDS words per lane of a traversal stack of depth STACK: child refs and entry distances.
 // (stack_lds_entries(STACK) entries: the LDS budget stays STACK words, so the
 // occupancy does not change; deeper entries spill to private memory)
-constexpr int stack_words(int STACK) { return STACK ? STACK : 1; }
+// (odd STACK: the 8-wide tree, STACK & ~1 LDS words per lane)
+constexpr int stack_words(int STACK) { return STACK ? (STACK & ~1) : 1; }
 
 // BVH::rayIntersect (bvh.cpp:404-462): adaptive epsilon, closest or any hit.
 // Near child first; the short stack lives in LDS, one column per lane.
@@ -456,7 +457,54 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     } flush{tstat};
 #endif
     for (;;) {
-        if (!(ref & 0x80000000u)) {
+        if (!(ref & 0x80000000u) && (STACK & 1)) {
+            // 8-wide node (odd STACK): 16 float4 = 256 B, the child boxes
+            // in SoA form (min.x of children 0-3 | 4-7, min.y, ..., max.z),
+            // the refs of children 0-3 | 4-7, padding.  The hit children are
+            // ordered by entry distance with Batcher's 19-comparator network on
+            // (sortable key bits, ref); misses carry the largest key and sort last.
+            NORI_TSTAT(0, 1);
+            const float4 *nd = S.nodes + 16 * (size_t)ref;
+            float4 v[14];
+#pragma unroll
+            for (int j = 0; j < 14; ++j) v[j] = gld(nd + j);
+            uint32_t kk[8], cc[8];
+            int nh = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int h = i >> 2, e = i & 3;
+                auto el = [e](const float4 &f) { return e == 0 ? f.x : e == 1 ? f.y : e == 2 ? f.z : f.w; };
+                float k;
+                const bool hit = box_test(make_float4(el(v[h]), el(v[2 + h]), el(v[4 + h]), 0),
+                                          make_float4(el(v[6 + h]), el(v[8 + h]), el(v[10 + h]), 0), r, k);
+                const uint32_t kb = __float_as_uint(k);
+                kk[i] = hit ? ((kb & 0x80000000u) ? ~kb : (kb | 0x80000000u)) : 0xFFFFFFFFu;
+                cc[i] = __float_as_uint(el(v[12 + h]));
+                nh += hit ? 1 : 0;
+            }
+            if (nh > 0) {
+                auto cs = [&](int a, int b) {
+                    const bool sw = kk[b] < kk[a];
+                    const uint32_t ka = kk[a], ca = cc[a];
+                    kk[a] = sw ? kk[b] : ka;
+                    kk[b] = sw ? ka : kk[b];
+                    cc[a] = sw ? cc[b] : ca;
+                    cc[b] = sw ? ca : cc[b];
+                };
+                cs(0, 1); cs(2, 3); cs(4, 5); cs(6, 7);
+                cs(0, 2); cs(1, 3); cs(4, 6); cs(5, 7);
+                cs(1, 2); cs(5, 6);
+                cs(0, 4); cs(1, 5); cs(2, 6); cs(3, 7);
+                cs(2, 4); cs(3, 5);
+                cs(1, 2); cs(3, 4); cs(5, 6);
+                auto unkey = [](uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); };
+#pragma unroll
+                for (int i = 7; i >= 1; --i)
+                    if (i < nh) push(sp, cc[i], unkey(kk[i]));
+                ref = cc[0];
+                continue;
+            }
+        } else if (!(ref & 0x80000000u)) {
             NORI_TSTAT(0, 1);
             float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
             load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
@@ -2639,6 +2687,7 @@ static void photons_dispatch(const DevScene &S, uint64_t e0, uint32_t n, uint32_
     case 0: hipLaunchKernelGGL((k_photons<0, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     case 8: hipLaunchKernelGGL((k_photons<8, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     case 16: hipLaunchKernelGGL((k_photons<16, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
+    case 17: hipLaunchKernelGGL((k_photons<17, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     default: hipLaunchKernelGGL((k_photons<32, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     }
 }
@@ -2652,6 +2701,12 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 
 #endif
 // ------------------------------------------------------------------ film splat
+#ifndef NORI_SPLAT2
+#define NORI_SPLAT2 0
+#endif
+#ifndef NORI_SPLAT2_WAVES
+#define NORI_SPLAT2_WAVES 4  // k_splat2: at most 128 VGPRs
+#endif
 #ifndef NORI_SPLAT_DEPTH
 #define NORI_SPLAT_DEPTH 1  // sample records in flight per thread (prefetch depth)
 #endif
@@ -2782,6 +2837,149 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
     }
 }
 
+// k_splat with a pixel's window split over two lanes by channel (NORI_SPLAT2):
+// lane 2i accumulates R and G, lane 2i+1 B and W of the same pixel, so each
+// holds 5 x 5 x 2 sums instead of 5 x 5 x 4 (k_splat's 256 VGPRs allow one
+// wave per SIMD, issuing at half rate with every latency exposed).  The pass
+// loop takes the pixel's samples two at a time: each lane regenerates the
+// jitter and the filter weights of one of them (lane parity = which) and the
+// pair swaps weights with one DPP move per value, so the per-sample work is
+// not doubled.  Every product and sum is the one k_splat computes, in the
+// same order per cell: ((L_c * wx) * wy) added pass by pass.
+ND float pair_swap(float v) {  // the partner lane's value (lanes 2i <-> 2i+1): DPP quad_perm [1, 0, 3, 2]
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+template <int B>
+__global__ __launch_bounds__(kSplatBlock) __attribute__((amdgpu_waves_per_eu(B <= 2 ? NORI_SPLAT2_WAVES : 1))) void k_splat2(DevScene S, const float4 *rec, SplatDesc sd, float *film,
+                                                       Counters *C) {
+    constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1;
+    __shared__ float tile[TS * TS * 4];
+    __shared__ float ftab[NORI_FILTER_RESOLUTION + 1];
+    int4 bi = sd.blocks[blockIdx.x];
+    const int ox = bi.x, oy = bi.y, bw = bi.z & 0xFFFF, bh = bi.z >> 16;
+    const uint32_t off = (uint32_t)bi.w;
+    const uint32_t p0 = blockIdx.y * sd.passes_per_wg, p1 = min(sd.passes, p0 + sd.passes_per_wg);
+    for (int i = threadIdx.x; i < TS * TS * 4; i += kSplatBlock) tile[i] = 0.0f;
+    if (threadIdx.x <= NORI_FILTER_RESOLUTION) ftab[threadIdx.x] = S.filter[threadIdx.x];
+    __syncthreads();
+    const int npix = bw * bh;
+    const float rad = S.filter_radius, lk = S.lookup;
+    const uint64_t WH = (uint64_t)S.W * (uint64_t)S.H;
+    const uint32_t ch = threadIdx.x & 1u;  // 0: R, G   1: B, W
+    uint32_t inval = 0;
+    // pixel rounds: the whole block iterates together so the DPP partners stay converged
+    for (int j0 = 0; j0 < npix; j0 += kSplatBlock / 2) {
+        const int j = j0 + (int)(threadIdx.x >> 1);
+        const bool pix = j < npix;
+        const int jj = pix ? j : 0;
+        const int ly = jj / bw, lx = jj - ly * bw, x = ox + lx, y = oy + ly;
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 acc[K][K];
+#pragma unroll
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int c = 0; c < K; ++c) acc[a][c] = f2{0.0f, 0.0f};
+        bool any = false;
+        float vs[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t p = p0; p < p1; p += 2) {
+            // the two samples of this pass pair, and this lane's one of them
+            float4 Ls[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                Ls[s] = pix && p + s < p1 ? rec[(size_t)(p + s) * sd.M + off + jj] : make_float4(0, 0, 0, 1);
+            const float4 L = ch ? Ls[1] : Ls[0];
+            bool use = L.w == 0.0f;  // not pending (the finisher splats pending samples)
+            const bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
+            if (use && !valid) ++inval;
+            use = use && valid;
+            float wx[K], wy[K];
+            {
+                uint64_t sid = (uint64_t)(sd.pass_begin + p + ch) * WH + (uint64_t)y * S.W + x;
+                Pcg r;
+                wave_seed(r, sd.seed, sid);
+                V2 jit = next2D(r);
+                float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
+                int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
+                int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
+#pragma unroll
+                for (int d = 0; d < K; ++d) {
+                    int cx = lx + d, cy = ly + d;
+                    int kx = min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION);
+                    int ky = min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION);
+                    const float fx = ftab[kx], fy = ftab[ky];
+                    wx[d] = (cx >= x0 && cx <= x1) ? fx : 0.0f;
+                    wy[d] = (cy >= y0 && cy <= y1) ? fy : 0.0f;
+                }
+            }
+            // the partner's weights and flag: sample 1 - ch
+            float ox_[K], oy_[K];
+#pragma unroll
+            for (int d = 0; d < K; ++d) {
+                ox_[d] = pair_swap(wx[d]);
+                oy_[d] = pair_swap(wy[d]);
+            }
+            const bool ouse = pair_swap(use ? 1.0f : 0.0f) != 0.0f;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const bool u = s == (int)ch ? use : ouse;
+                if (!u) continue;
+                const float4 Lq = Ls[s];
+                any = true;
+                if (ch == 0) {
+                    vs[0] += Lq.x;
+                    vs[1] += Lq.y;
+                    vs[2] += Lq.z;
+                    vs[3] += Lq.x * Lq.x;
+                    vs[4] += Lq.y * Lq.y;
+                    vs[5] += Lq.z * Lq.z;
+                    vs[6] += 1.0f;
+                }
+                const f2 Lc = ch ? f2{Lq.z, 1.0f} : f2{Lq.x, Lq.y};
+                f2 lw[K];
+#pragma unroll
+                for (int c = 0; c < K; ++c) lw[c] = Lc * (s == (int)ch ? wx[c] : ox_[c]);
+#pragma unroll
+                for (int a = 0; a < K; ++a) {
+                    const float wa = s == (int)ch ? wy[a] : oy_[a];
+#pragma unroll
+                    for (int c = 0; c < K; ++c) acc[a][c] += lw[c] * wa;
+                }
+            }
+        }
+        if (any && pix && ch == 0 && sd.var) {
+            float *v = sd.var + 8 * ((size_t)y * S.W + x);
+            for (int k = 0; k < 7; ++k) atomicAdd(v + k, vs[k]);
+        }
+        if (any && pix) {
+#pragma unroll
+            for (int a = 0; a < K; ++a)
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    float *t = tile + 4 * ((ly + a) * TS + (lx + c)) + 2 * ch;
+                    const f2 v = acc[a][c];
+                    if (v.x != 0.0f || v.y != 0.0f) {
+                        atomicAdd(t + 0, v.x);
+                        atomicAdd(t + 1, v.y);
+                    }
+                }
+        }
+    }
+    if (inval) atomicAdd(&C->invalid, (unsigned long long)inval);
+    __syncthreads();
+    const int rows = bh + 2 * B, cols = bw + 2 * B, FW = S.W + 2 * B;
+    for (int i = threadIdx.x; i < rows * cols; i += kSplatBlock) {
+        int yy = i / cols, xx = i - yy * cols;
+        const float *c = tile + 4 * (yy * TS + xx);
+        float *f = film + 4 * ((size_t)(oy + yy) * FW + (ox + xx));
+        if (c[3] != 0.0f || c[0] != 0.0f || c[1] != 0.0f || c[2] != 0.0f) {
+            atomicAdd(f + 0, c[0]);
+            atomicAdd(f + 1, c[1]);
+            atomicAdd(f + 2, c[2]);
+            atomicAdd(f + 3, c[3]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 #if NORI_TU == 0
 template <bool ANY>
@@ -2792,6 +2990,7 @@ static hipError_t trace_dispatch(const DevScene &S, const float4 *rays, uint32_t
     case 0: hipLaunchKernelGGL((k_trace<0, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 8: hipLaunchKernelGGL((k_trace<8, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 16: hipLaunchKernelGGL((k_trace<16, ANY>), g, b, 0, st, S, rays, n, hits); break;
+    case 17: hipLaunchKernelGGL((k_trace<17, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 32: hipLaunchKernelGGL((k_trace<32, ANY>), g, b, 0, st, S, rays, n, hits); break;
     default: hipLaunchKernelGGL((k_trace<64, ANY>), g, b, 0, st, S, rays, n, hits); break;
     }
@@ -2875,6 +3074,7 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
     switch (stack) {
     case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt, G); break;
     case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, cnt, G); break;
+    case 17: hipLaunchKernelGGL(k_extend<17>, g, b, 0, st, S, q, cnt, G); break;
     case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, cnt, G); break;
     default: hipLaunchKernelGGL(k_extend<64>, g, b, 0, st, S, q, cnt, G); break;
     }
@@ -2892,6 +3092,7 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     switch (stack) {
     case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec, G); break;
+    case 17: hipLaunchKernelGGL(k_shadow<17>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     }
@@ -2943,6 +3144,7 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
         break;
     case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
+    case 17: hipLaunchKernelGGL((k_finish<17, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     default: hipLaunchKernelGGL((k_finish<64, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
@@ -2977,6 +3179,7 @@ static void direct_dispatch(const DevScene &S, const WorkDesc &wd, float4 *rec, 
     case 0: hipLaunchKernelGGL((k_direct<0, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     case 8: hipLaunchKernelGGL((k_direct<8, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     case 16: hipLaunchKernelGGL((k_direct<16, INTEG>), g, b, 0, st, S, wd, rec, C); break;
+    case 17: hipLaunchKernelGGL((k_direct<17, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     default: hipLaunchKernelGGL((k_direct<32, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     }
 }
@@ -3032,6 +3235,21 @@ hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &s
                         Counters *C, hipStream_t st) {
     if (nblocks == 0 || sd.passes == 0) return hipSuccess;
     dim3 g(nblocks, (sd.passes + sd.passes_per_wg - 1) / sd.passes_per_wg), b(kSplatBlock);
+    static const bool two = [] {
+        const char *e = std::getenv("NORI_SPLAT2");
+        return e ? e[0] == '1' : NORI_SPLAT2 != 0;
+    }();
+    if (two) {
+        switch (S.border) {
+        case 0: hipLaunchKernelGGL(k_splat2<0>, g, b, 0, st, S, rec, sd, film, C); break;
+        case 1: hipLaunchKernelGGL(k_splat2<1>, g, b, 0, st, S, rec, sd, film, C); break;
+        case 2: hipLaunchKernelGGL(k_splat2<2>, g, b, 0, st, S, rec, sd, film, C); break;
+        case 3: hipLaunchKernelGGL(k_splat2<3>, g, b, 0, st, S, rec, sd, film, C); break;
+        case 4: hipLaunchKernelGGL(k_splat2<4>, g, b, 0, st, S, rec, sd, film, C); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (S.border) {
     case 0: hipLaunchKernelGGL(k_splat<0>, g, b, 0, st, S, rec, sd, film, C); break;
     case 1: hipLaunchKernelGGL(k_splat<1>, g, b, 0, st, S, rec, sd, film, C); break;
