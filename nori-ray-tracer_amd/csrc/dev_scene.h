@@ -74,6 +74,7 @@ struct DevScene {
     uint32_t num_nodes;
     uint32_t num_prims;
     uint32_t num_scan_tris;  // scan mode: prims = triangles (padded to kScanGroup), then spheres
+    uint32_t num_scan_real;  // scan mode: triangle records before the padding of the last group
     // scan mode: axis-plane triangle pairs (runtime.hip build_scan_list):
     // pair g = scan records 2g, 2g+1 in the plane x_a = plane_c[g], pairs of
     // axis a are [plane_end[a-1], plane_end[a])

@@ -324,7 +324,7 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
         scan_planes<1, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<2, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
     }
-    const uint32_t nt = S.num_scan_tris, n = S.num_prims;
+    const uint32_t nt = S.num_scan_tris, n = S.num_prims, real = S.num_scan_real;
     for (uint32_t i = 2 * S.plane_end[2]; i < nt; i += kScanGroup) {
         if (ANY && all_done()) return;
         const float4 *p = S.prims + 3 * (size_t)i;
@@ -333,7 +333,8 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
         for (uint32_t j = 0; j < 3 * kScanGroup; ++j) q[j] = p[j];
 #pragma unroll
         for (uint32_t g = 0; g < kScanGroup; ++g)
-            scan_tri<K, ANY>(q[3 * g], q[3 * g + 1], q[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
+            if (i + g < real)  // (the padding records never hit)
+                scan_tri<K, ANY>(q[3 * g], q[3 * g + 1], q[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
     for (uint32_t i = nt; i < n; ++i) {
         if (ANY && all_done()) return;
@@ -984,7 +985,8 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
         for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
 #pragma unroll
         for (uint32_t g = 0; g < kScanGroup; ++g)
-            scan_tri<1, false>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
+            if (k + g < S.num_scan_real)  // (the padding records never hit)
+                scan_tri<1, false>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
     for (uint32_t k = nt + ns; k < nall; ++k) sphere_own(k, live[0]);  // (NORI_BIN_SPHERES=0)
     __syncthreads();

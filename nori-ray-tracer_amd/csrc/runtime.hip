@@ -391,6 +391,7 @@ struct ScanList {
     std::vector<float> plane_f; // per pair: the in-plane filter of k_extend_bin (8 floats, plane_filters)
     uint32_t plane_end[3] = {0, 0, 0};  // pairs with axis <= a
     uint32_t tris = 0;          // triangle records (pairs + the rest, padded)
+    uint32_t real = 0;          // ... of which the last real one ends here (the padding after it never hits)
 };
 
 // The in-plane filter of the binned extension kernel (kernels.hip
@@ -533,6 +534,7 @@ ScanList build_scan_list(const DeviceBvh &bvh, uint32_t n) {
     uint32_t rest = 0;
     for (uint32_t i = 0; i < n; ++i)
         if (!sphere(i) && axis[i] < 0) add(i), ++rest;
+    L.real = L.tris + rest;
     for (; rest % kScanGroup; ++rest) add_null();
     L.tris += rest;
     for (uint32_t i = 0; i < n; ++i)
@@ -547,6 +549,7 @@ ScanList build_scan_list(const DeviceBvh &bvh, uint32_t n) {
                 std::memcpy(&F.prims[F.prims.size() - 1], &i, 4);
                 ++F.tris;
             }
+        F.real = F.tris;
         for (; F.tris % kScanGroup; ++F.tris) {
             float null_prim[12] = {0};
             const uint32_t none = 0xFFFFFFFFu;
@@ -873,6 +876,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.num_nodes = bvh.num_nodes;
     S.num_prims = (uint32_t)(prim_list.size() / 12);
     S.num_scan_tris = scan_list.tris;
+    S.num_scan_real = scan_list.real;
     S.plane_c = scan_list.plane_c.empty() ? nullptr : c.plane_c.as<float>();
     S.plane_f = scan_list.plane_f.empty() ? nullptr : c.plane_f.as<float4>();
     for (int a = 0; a < 3; ++a) S.plane_end[a] = scan_list.plane_end[a];
