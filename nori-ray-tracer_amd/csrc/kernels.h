@@ -81,8 +81,9 @@ hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &s
                         Counters *C, hipStream_t st);
 
 bool trav_stats_take(unsigned long long out[8]);  // NORI_TRAV_STATS builds (diagnostic)
-// Scan-mode extension kernel: 1 k_extend_bin, 0 k_extend_scan, 2 both, compared
-// (NORI_EXTEND_CHECK=1); extend_check_take reads and resets (mismatches, compared).
+// Scan-mode trace kernels: 1 k_trace_bin, 0 k_extend_scan / k_shadow_scan, 2
+// both, compared (NORI_EXTEND_CHECK=1); extend_check_take reads and resets
+// (hit mismatches, compared extension rays, occlusion mismatches, compared shadow rays).
 int extend_mode();
-bool extend_check_take(unsigned long long out[2]);
+bool extend_check_take(unsigned long long out[4]);
 }  // namespace nori

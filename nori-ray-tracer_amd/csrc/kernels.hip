@@ -845,6 +845,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
 #ifndef NORI_BIN_SPHERES
 #define NORI_BIN_SPHERES 1
 #endif
+#ifndef NORI_SHADOW_BIN
+#define NORI_SHADOW_BIN 1
+#endif
 constexpr int kBinBlock = 256;
 constexpr uint32_t kBinSlices = kTraceGroup * kSeg / kBinBlock;  // work-groups per group of segments
 constexpr int kBinSlots = 3;
@@ -901,7 +904,13 @@ ND float sphere_disc(const float4 &a, const float4 &b, const TRay &r) {
 }
 
 #if NORI_TU == 0
-__global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
+// ANY = false: closest hit of the path queue's extension rays (k_extend_scan's
+// results).  ANY = true: the shadow queue's rays, any hit; an unoccluded ray
+// adds its payload to its sample record (k_shadow_scan), or with FLAGS its
+// occlusion to flags[entry] (NORI_EXTEND_CHECK).
+template <bool ANY, bool FLAGS>
+__global__ __launch_bounds__(kBinBlock) void k_trace_bin(DevScene S, PathQueue pq, ShadowQueue sq, const uint32_t *cnt,
+                                                         uint32_t G, float4 *rec, uint32_t *flags) {
     constexpr uint32_t NW = kBinBlock / 64, CAP = 64 * kBinSlots;
     __shared__ float4 s_ray[2][kBinBlock];              // (o, mint), (d, maxt)
     __shared__ float4 s_res[kBinSlots][kBinBlock];      // per (slot, ray): t, u, v, prim | pos << 16
@@ -920,20 +929,48 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
     const uint32_t q = seg_entry(sr, valid ? i : i0);
     TRay r[1];
     bool live[1] = {valid};
-    path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
+    float4 pay = make_float4(0, 0, 0, 0);
+    if constexpr (ANY) {
+        const float4 a = sq.ray_o[q], b = sq.ray_d[q];
+        if (!FLAGS) pay = sq.payload[q];  // fetched now: its latency hides behind the tests
+        r[0].o = ld3(a);
+        r[0].d = ld3(b);
+        r[0].mint = a.w;
+        r[0].maxt = b.w;
+    } else {
+        path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
+    }
     scan_prologue<1>(S, r, live);
+    float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
+    uint32_t pb[1] = {0xFFFFFFFFu}, lb[1] = {0u};
+    bool found[1] = {false};
+    // the ray's own tests of the triangles outside the pairs (scan_core's
+    // loop); a closest-hit ray's maxt shrinks to its hit, so farther
+    // candidates are not handed out; an occluded shadow ray hands out none
+    for (uint32_t k = 2 * np; k < nt; k += kScanGroup) {
+        if (ANY && !__any(live[0] && !found[0])) break;
+        const float4 *p = S.prims + 3 * (size_t)k;
+        float4 qq[3 * kScanGroup];
+#pragma unroll
+        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
+#pragma unroll
+        for (uint32_t g = 0; g < kScanGroup; ++g)
+            if (k + g < S.num_scan_real)  // (the padding records never hit)
+                scan_tri<1, ANY>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
+    }
+    const bool open = live[0] && !(ANY && found[0]);
     // (1) candidates
     BinCand bc;
     {
         const float mlo = r[0].mint > 0.0f ? r[0].mint * kPlaneLo : -INF_F;
         const float mhi = r[0].maxt > 0.0f ? r[0].maxt * kPlaneHi : INF_F;
-        bin_axis<0>(S, r[0], live[0], mlo, mhi, bc);
-        bin_axis<1>(S, r[0], live[0], mlo, mhi, bc);
-        bin_axis<2>(S, r[0], live[0], mlo, mhi, bc);
+        bin_axis<0>(S, r[0], open, mlo, mhi, bc);
+        bin_axis<1>(S, r[0], open, mlo, mhi, bc);
+        bin_axis<2>(S, r[0], open, mlo, mhi, bc);
     }
     for (uint32_t k = 0; k < ns; ++k) {
         const float4 *p = S.prims + 3 * (size_t)(nt + k);
-        if (live[0] && sphere_disc(p[0], p[1], r[0]) > 0.0f) bc.add(128u | k);
+        if (open && sphere_disc(p[0], p[1], r[0]) > 0.0f) bc.add(128u | k);
     }
     const bool dense = bc.n > (uint32_t)kBinSlots;
     const uint32_t m = dense ? 0u : bc.n;
@@ -953,40 +990,29 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
         }
         if (lane == 0) s_nitem[kind][w] = (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
     }
-    // the ray's own tests: every pair and sphere for a dense ray, then the
-    // other triangles (scan_core's loops)
-    float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
-    uint32_t pb[1] = {0xFFFFFFFFu}, lb[1] = {0u};
-    bool found[1] = {false};
+    // a dense ray tests every pair and sphere itself
     auto sphere_own = [&](uint32_t k, bool on) {
         const float4 *p = S.prims + 3 * (size_t)k;
         const float4 p0 = p[0], p1 = p[1];
         const uint32_t pos = __float_as_uint(p[2].w);
         float t = 0;
         const bool h = sphere_hit_nb(p0, p1, r[0], t);  // t <= r.maxt = tb
-        if (h && on && (t != tb[0] || pos > lb[0])) {
-            r[0].maxt = tb[0] = t;
-            ub[0] = vb[0] = 0.0f;
-            pb[0] = __float_as_uint(p0.w);
-            lb[0] = pos;
+        if (h && on && (ANY || t != tb[0] || pos > lb[0])) {
+            found[0] = true;
+            if (!ANY) {
+                r[0].maxt = tb[0] = t;
+                ub[0] = vb[0] = 0.0f;
+                pb[0] = __float_as_uint(p0.w);
+                lb[0] = pos;
+            }
         }
     };
     if (__any(dense)) {
-        bool dl[1] = {dense && live[0]};
-        scan_planes<0, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
-        scan_planes<1, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
-        scan_planes<2, 1, false, false>(S, r, dl, tb, pb, lb, ub, vb, found);
+        bool dl[1] = {dense && open};
+        scan_planes<0, 1, ANY, ANY>(S, r, dl, tb, pb, lb, ub, vb, found);
+        scan_planes<1, 1, ANY, ANY>(S, r, dl, tb, pb, lb, ub, vb, found);
+        scan_planes<2, 1, ANY, ANY>(S, r, dl, tb, pb, lb, ub, vb, found);
         for (uint32_t k = nt; k < nt + ns; ++k) sphere_own(k, dl[0]);
-    }
-    for (uint32_t k = 2 * np; k < nt; k += kScanGroup) {
-        const float4 *p = S.prims + 3 * (size_t)k;
-        float4 qq[3 * kScanGroup];
-#pragma unroll
-        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
-#pragma unroll
-        for (uint32_t g = 0; g < kScanGroup; ++g)
-            if (k + g < S.num_scan_real)  // (the padding records never hit)
-                scan_tri<1, false>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
     for (uint32_t k = nt + ns; k < nall; ++k) sphere_own(k, live[0]);  // (NORI_BIN_SPHERES=0)
     __syncthreads();
@@ -1026,9 +1052,10 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
                     const float4 a = p[3 * e], b = p[3 * e + 1], c = p[3 * e + 2];
                     float t = 0, u = 0, v = 0;
                     const uint32_t pos = __float_as_uint(c.w);
-                    if (tri_hit_nb(a, b, c, x, t, u, v) && (t != res.x || pos > lpos)) {
-                        res = make_float4(t, u, v, __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | pos << 16));
-                        x.maxt = t;
+                    if (tri_hit_nb(a, b, c, x, t, u, v) && (ANY || t != res.x || pos > lpos)) {
+                        res = ANY ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
+                                  : make_float4(t, u, v, __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | pos << 16));
+                        if (!ANY) x.maxt = t;
                         lpos = pos;
                     }
                 }
@@ -1037,8 +1064,9 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
                 const float4 a = p[0];
                 float t = 0;
                 if (sphere_hit_nb(a, p[1], x, t))
-                    res = make_float4(t, 0.0f, 0.0f,
-                                      __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | __float_as_uint(p[2].w) << 16));
+                    res = ANY ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
+                              : make_float4(t, 0.0f, 0.0f,
+                                            __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | __float_as_uint(p[2].w) << 16));
             }
             s_res[slot][rid] = res;
         }
@@ -1050,7 +1078,9 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
         if ((uint32_t)e < m) {
             const float4 res = s_res[e][tid];
             const uint32_t wd = __float_as_uint(res.w), pos = wd >> 16;
-            if (res.x < tb[0] || (res.x == tb[0] && pos > lb[0])) {
+            if (ANY) {
+                found[0] = found[0] || res.x == 0.0f;
+            } else if (res.x < tb[0] || (res.x == tb[0] && pos > lb[0])) {
                 tb[0] = res.x;
                 ub[0] = res.y;
                 vb[0] = res.z;
@@ -1059,12 +1089,16 @@ __global__ __launch_bounds__(kBinBlock) void k_extend_bin(DevScene S, PathQueue 
             }
         }
     }
-    if (valid) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
+    if (!valid) return;
+    if constexpr (!ANY) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
+    else if constexpr (FLAGS) flags[q] = found[0] ? 1u : 0u;
+    else if (!found[0]) shadow_add(rec, pay);
 }
 
 // NORI_EXTEND_CHECK (diagnostic): mismatching hit records between the two
-// extension kernels on the same queue (t and prim bitwise, u and v as values).
-__device__ unsigned long long g_extend_check[2];
+// extension kernels on the same queue (t and prim bitwise, u and v as values),
+// and mismatching occlusion between the two shadow kernels.
+__device__ unsigned long long g_extend_check[4];
 __global__ __launch_bounds__(kTraceBlock) void k_extend_cmp(const float4 *a, const float4 *b, const uint32_t *cnt,
                                                             uint32_t G) {
     const uint32_t e = blockIdx.x * kTraceBlock + threadIdx.x, s = e / kSeg;
@@ -1074,6 +1108,28 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_cmp(const float4 *a, con
                       x.z == y.z && x.w == y.w;
     atomicAdd(&g_extend_check[1], 1ull);
     if (!same) atomicAdd(&g_extend_check[0], 1ull);
+}
+// the occlusion k_shadow_scan finds for every shadow ray (scan_rays, one ray
+// per thread), compared with k_trace_bin<true, true>'s flags
+__global__ __launch_bounds__(kTraceBlock) void k_shadow_cmp(DevScene S, ShadowQueue sq, const uint32_t *cnt, uint32_t G,
+                                                            const uint32_t *flags) {
+    const uint32_t e = blockIdx.x * kTraceBlock + threadIdx.x, s = e / kSeg;
+    const bool ok = s < G && e % kSeg < cnt[s < G ? s : 0];
+    if (!__any(ok)) return;
+    const uint32_t q = ok ? e : (s < G ? s * kSeg : 0u);
+    const float4 a = sq.ray_o[q], b = sq.ray_d[q];
+    TRay r[1];
+    r[0].o = ld3(a);
+    r[0].d = ld3(b);
+    r[0].mint = a.w;
+    r[0].maxt = b.w;
+    bool live[1] = {ok}, f[1];
+    float t[1], u[1], v[1];
+    uint32_t p[1];
+    scan_rays<1, true>(S, r, live, t, p, u, v, f);
+    if (!ok) return;
+    atomicAdd(&g_extend_check[3], 1ull);
+    if ((flags[q] != 0u) != f[0]) atomicAdd(&g_extend_check[2], 1ull);
 }
 #endif
 
@@ -3044,6 +3100,31 @@ hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue 
 
 #endif
 #if NORI_TU == 0
+// The binned kernels need every staged record in kBinMaxRec.
+static bool bin_ok(const DevScene &S) {
+    return S.plane_f && 2 * S.plane_end[2] + (S.num_prims - S.num_scan_tris) <= kBinMaxRec;
+}
+// Shadow rays through k_trace_bin<true> (NORI_SHADOW_BIN=0: k_shadow_scan).
+static bool shadow_bin() {
+    static const bool on = [] {
+        const char *e = std::getenv("NORI_SHADOW_BIN");
+        return e ? e[0] != '0' : NORI_SHADOW_BIN != 0;
+    }();
+    return on;
+}
+// Diagnostic scratch of NORI_EXTEND_CHECK (grown as needed, never freed).
+static float4 *check_scratch(size_t bytes) {
+    static float4 *p = nullptr;
+    static size_t have = 0;
+    if (have < bytes) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        have = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        have = bytes;
+    }
+    return p;
+}
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
@@ -3051,25 +3132,19 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
         const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
         const int mode = extend_mode();
-        const bool bin_ok = S.plane_f && 2 * S.plane_end[2] + (S.num_prims - S.num_scan_tris) <= kBinMaxRec;
-        if (mode == 1 && bin_ok) {
-            hipLaunchKernelGGL(k_extend_bin, gb, bb, 0, st, S, q, cnt, G);
+        const ShadowQueue nsq{nullptr, nullptr, nullptr};
+        if (mode == 1 && bin_ok(S)) {
+            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
             return hipGetLastError();
         }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
-        if (mode == 2 && bin_ok) {  // NORI_EXTEND_CHECK
-            static float4 *scratch = nullptr;
-            static size_t have = 0;
-            const size_t need = (size_t)G * kSeg;
-            if (have < need) {
-                if (scratch) (void)hipFree(scratch);
-                if (hipMalloc(&scratch, need * sizeof(float4)) != hipSuccess) return hipErrorOutOfMemory;
-                have = need;
-            }
+        if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK
+            float4 *scratch = check_scratch((size_t)G * kSeg * sizeof(float4));
+            if (!scratch) return hipErrorOutOfMemory;
             PathQueue q2 = q;
             q2.hit = scratch;
-            hipLaunchKernelGGL(k_extend_bin, gb, bb, 0, st, S, q2, cnt, G);
-            hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)(need / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
+            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
+            hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
         }
         return hipGetLastError();
     }
@@ -3088,6 +3163,19 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRaysShadow));
+        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
+        const int mode = extend_mode();
+        const PathQueue npq{nullptr, nullptr, nullptr, nullptr, nullptr};
+        if (mode == 1 && bin_ok(S) && shadow_bin()) {
+            hipLaunchKernelGGL((k_trace_bin<true, false>), gb, bb, 0, st, S, npq, sq, shcnt, G, rec, nullptr);
+            return hipGetLastError();
+        }
+        if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK: the occlusion of both kernels, before the record update
+            uint32_t *flags = reinterpret_cast<uint32_t *>(check_scratch((size_t)G * kSeg * sizeof(float4)));
+            if (!flags) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL((k_trace_bin<true, true>), gb, bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
+            hipLaunchKernelGGL(k_shadow_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, S, sq, shcnt, G, flags);
+        }
         hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, b, 0, st, S, sq, shcnt, rec, G);
         return hipGetLastError();
     }
@@ -3200,7 +3288,7 @@ hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Cou
     return hipGetLastError();
 }
 
-// The scan-mode extension kernel: 1 k_extend_bin (default), 0 k_extend_scan
+// The scan-mode trace kernels: 1 k_trace_bin (default), 0 k_extend_scan / k_shadow_scan
 // (NORI_EXTEND_BIN=0), 2 both on every launch, compared (NORI_EXTEND_CHECK=1).
 int extend_mode() {
     static const int mode = [] {
@@ -3213,10 +3301,10 @@ int extend_mode() {
     return mode;
 }
 // NORI_EXTEND_CHECK: read (and reset) the mismatch and compared-entry counts.
-bool extend_check_take(unsigned long long out[2]) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_extend_check), 2 * sizeof(unsigned long long)) != hipSuccess)
+bool extend_check_take(unsigned long long out[4]) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_extend_check), 4 * sizeof(unsigned long long)) != hipSuccess)
         return false;
-    unsigned long long z[2] = {0, 0};
+    unsigned long long z[4] = {0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_extend_check), z, sizeof(z)) == hipSuccess;
 }
 

@@ -1003,6 +1003,7 @@ bool debug_log() {
 // 3089; C4 and C5 within 1 %).
 uint32_t pool_parts(bool bvh) {
     (void)bvh;
+    if (extend_mode() == 2) return 1u;  // NORI_EXTEND_CHECK: its scratch serves one stream
     const uint32_t def = 3u;
     const char *e = std::getenv("NORI_POOL_PARTS");
     const long v = e ? std::atol(e) : (long)def;
@@ -1453,11 +1454,16 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         invalid += hc.invalid;
         if (c.stack == 0 && extend_mode() == 2) {  // NORI_EXTEND_CHECK: the two extension kernels must agree
-            unsigned long long ck[2] = {0, 0};
-            if (extend_check_take(ck) && (debug_log() || ck[0]))
+            unsigned long long ck[4] = {0, 0, 0, 0};
+            if (extend_check_take(ck) && (debug_log() || ck[0] || ck[2])) {
                 std::fprintf(stderr, "[nori] extension check: %llu of %llu hit records differ\n", ck[0], ck[1]);
-            if (ck[0]) throw NoriException(NORI_ERR_INVALID, "extension check: k_extend_bin and k_extend_scan differ on " +
-                                                              std::to_string(ck[0]) + " of " + std::to_string(ck[1]) + " rays");
+                std::fprintf(stderr, "[nori] shadow check: %llu of %llu occlusions differ\n", ck[2], ck[3]);
+            }
+            if (ck[0] || ck[2])
+                throw NoriException(NORI_ERR_INVALID, "trace check: k_trace_bin differs from the scan on " +
+                                                          std::to_string(ck[0]) + " of " + std::to_string(ck[1]) +
+                                                          " extension rays and " + std::to_string(ck[2]) + " of " +
+                                                          std::to_string(ck[3]) + " shadow rays");
         }
         if (debug_log())
         {

@@ -1,10 +1,11 @@
-"""GPU: the binned extension kernel (kernels.hip k_extend_bin, the default for
+"""GPU: the binned trace kernel (kernels.hip k_trace_bin, the default for
 scan-mode scenes with axis-plane pairs) returns exactly the hits of the
-per-lane scan k_extend_scan.  With NORI_EXTEND_CHECK=1 every extension launch
-of a render runs both kernels on the same queue and compares the hit records
-(t and primitive bitwise, u and v as values); the render fails on any
-difference.  Each scene renders in its own process (the kernel choice is read
-once per process)."""
+per-lane scans: closest hits as k_extend_scan, shadow-ray occlusion as
+k_shadow_scan.  With NORI_EXTEND_CHECK=1 every extension and shadow launch of
+a render runs both kernels on the same queue and compares the hit records (t
+and primitive bitwise, u and v as values) and the occlusion of every shadow
+ray; the render fails on any difference.  Each scene renders in its own
+process (the kernel choice is read once per process)."""
 import os
 import subprocess
 import sys
@@ -39,11 +40,12 @@ def test_bin_matches_scan(built, parts):
                PYTHONPATH=os.path.join(ROOT, "nori-ray-tracer_amd"))
     r = subprocess.run([sys.executable, "-c", SCRIPT, scene_path(*parts), "160", "120", "16"], env=env,
                        capture_output=True, text=True, timeout=300)
-    lines = [l for l in r.stderr.splitlines() if "extension check" in l]
+    lines = [l for l in r.stderr.splitlines() if "extension check" in l or "shadow check" in l]
     assert r.returncode == 0 and "rendered" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
     if not lines:
         pytest.skip("scene has no axis-plane pairs: k_extend_bin is not used")
     for l in lines:
         words = l.split()
         bad, total = int(words[words.index("of") - 1]), int(words[words.index("of") + 1])
-        assert bad == 0 and total > 10000, l
+        assert bad == 0 and total > 1000, l
+    assert any("shadow check" in l for l in lines) and any("extension check" in l for l in lines)
