@@ -323,7 +323,9 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
         }
     }
     uint32_t n = (uint32_t)prim_shape.size();
+    const uint32_t width = out.width;  // the caller's choice survives the reset
     out = DeviceBvh();
+    out.width = width;
     if (n == 0) throw NoriException(NORI_ERR_INVALID, "scene has no primitives");
     if (n >= (1u << 25)) throw NoriException(NORI_ERR_UNSUPPORTED, "more than 2^25 primitives");
     auto T0 = std::chrono::steady_clock::now();

@@ -918,27 +918,66 @@ __global__ __launch_bounds__(kBinBlock) void k_trace_bin(DevScene S, PathQueue p
     __shared__ uint16_t s_item[2][NW][CAP];             // per kind and wave: ray | index << 8 | slot << 14
     __shared__ uint32_t s_nitem[2][NW];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const SegRange sr = seg_range_k(cnt, G, kTraceSlices / kBinSlices);
-    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % kBinSlices) * kBinBlock, i = i0 + tid;
-    if (i0 >= n) return;  // the whole work-group: its slice is empty
     const uint32_t np = S.plane_end[2], nt = S.num_scan_tris, nall = S.num_prims;
     const uint32_t ns = NORI_BIN_SPHERES ? nall - nt : 0u, sph0 = 6 * np;
     for (uint32_t j = tid; j < 6 * np; j += kBinBlock) s_rec[j] = S.prims[j];
     for (uint32_t j = tid; j < 3 * ns; j += kBinBlock) s_rec[sph0 + j] = S.prims[3 * nt + j];
+    // The work-groups stride over the slices (256 queue entries of a group of
+    // segments): a grid of resident work-groups loops, and the next slice's
+    // rays are loaded while this one is tested, so the ray loads' latency
+    // hides behind the tests (a grid of one work-group per slice runs each
+    // body once).
+    const uint32_t nsl = (G + kTraceGroup - 1) / kTraceGroup * kBinSlices;
+    struct Fetch {
+        uint32_t n, i0, q;
+        float4 a, b, c;
+    };
+    auto fetch = [&](uint32_t sl) {
+        Fetch f;
+        f.n = 0;
+        f.i0 = 0;
+        f.q = 0;
+        if (sl >= nsl) return f;
+        SegRange sr;
+        sr.s0 = (sl / kBinSlices) * kTraceGroup;
+        sr.pre[0] = 0;
+#pragma unroll
+        for (int k = 0; k < kTraceGroup; ++k) sr.pre[k + 1] = sr.pre[k] + (sr.s0 + k < G ? cnt[sr.s0 + k] : 0u);
+        f.n = sr.pre[kTraceGroup];
+        f.i0 = (sl % kBinSlices) * kBinBlock;
+        if (f.i0 >= f.n) return f;  // an empty slice
+        const uint32_t i = f.i0 + tid;
+        f.q = seg_entry(sr, i < f.n ? i : f.i0);
+        if constexpr (ANY) {
+            f.a = sq.ray_o[f.q];
+            f.b = sq.ray_d[f.q];
+            if (!FLAGS) f.c = sq.payload[f.q];
+        } else {
+            f.a = pq.ray_o[f.q];
+            f.b = pq.ray_d[f.q];
+        }
+        return f;
+    };
+    Fetch cur = fetch(blockIdx.x);
+    for (uint32_t sl = blockIdx.x; sl < nsl; sl += gridDim.x) {
+    const Fetch nxt = fetch(sl + gridDim.x);
+    if (cur.i0 >= cur.n) {  // (uniform) nothing queued in this slice
+        cur = nxt;
+        continue;
+    }
+    const uint32_t n = cur.n, i = cur.i0 + tid, q = cur.q;
     const bool valid = i < n;
-    const uint32_t q = seg_entry(sr, valid ? i : i0);
     TRay r[1];
     bool live[1] = {valid};
     float4 pay = make_float4(0, 0, 0, 0);
     if constexpr (ANY) {
-        const float4 a = sq.ray_o[q], b = sq.ray_d[q];
-        if (!FLAGS) pay = sq.payload[q];  // fetched now: its latency hides behind the tests
-        r[0].o = ld3(a);
-        r[0].d = ld3(b);
-        r[0].mint = a.w;
-        r[0].maxt = b.w;
+        if (!FLAGS) pay = cur.c;
+        r[0].o = ld3(cur.a);
+        r[0].d = ld3(cur.b);
+        r[0].mint = cur.a.w;
+        r[0].maxt = cur.b.w;
     } else {
-        path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
+        path_ray(S, cur.a, cur.b, r[0]);
     }
     scan_prologue<1>(S, r, live);
     float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
@@ -1089,10 +1128,14 @@ __global__ __launch_bounds__(kBinBlock) void k_trace_bin(DevScene S, PathQueue p
             }
         }
     }
-    if (!valid) return;
-    if constexpr (!ANY) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
-    else if constexpr (FLAGS) flags[q] = found[0] ? 1u : 0u;
-    else if (!found[0]) shadow_add(rec, pay);
+    if (valid) {
+        if constexpr (!ANY) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
+        else if constexpr (FLAGS) flags[q] = found[0] ? 1u : 0u;
+        else if (!found[0]) shadow_add(rec, pay);
+    }
+    __syncthreads();  // the LDS lists and results are reused by the next slice
+    cur = nxt;
+    }
 }
 
 // NORI_EXTEND_CHECK (diagnostic): mismatching hit records between the two
@@ -3112,6 +3155,24 @@ static bool shadow_bin() {
     }();
     return on;
 }
+// Grid of a binned trace launch: the resident work-groups (occupancy x CUs,
+// queried once per kernel), which loop over the slices prefetching the next
+// one's rays; NORI_BIN_PERSIST=0: one work-group per slice.
+template <bool ANY, bool FLAGS>
+static dim3 bin_grid(uint32_t G) {
+    const uint32_t nsl = (G + kTraceGroup - 1) / kTraceGroup * kBinSlices;
+    static const uint32_t resident = [] {
+        const char *e = std::getenv("NORI_BIN_PERSIST");
+        if (e && e[0] == '0') return 0u;
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trace_bin<ANY, FLAGS>, kBinBlock, 0) != hipSuccess)
+            return 0u;
+        return (uint32_t)(cus * per);
+    }();
+    return dim3(resident ? std::min(nsl, resident) : nsl);
+}
 // Diagnostic scratch of NORI_EXTEND_CHECK (grown as needed, never freed).
 static float4 *check_scratch(size_t bytes) {
     static float4 *p = nullptr;
@@ -3130,11 +3191,11 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
-        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
+        const dim3 bb(kBinBlock);
         const int mode = extend_mode();
         const ShadowQueue nsq{nullptr, nullptr, nullptr};
         if (mode == 1 && bin_ok(S)) {
-            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
+            hipLaunchKernelGGL((k_trace_bin<false, false>), (bin_grid<false, false>(G)), bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
             return hipGetLastError();
         }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
@@ -3143,7 +3204,7 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
             if (!scratch) return hipErrorOutOfMemory;
             PathQueue q2 = q;
             q2.hit = scratch;
-            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
+            hipLaunchKernelGGL((k_trace_bin<false, false>), (bin_grid<false, false>(G)), bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
             hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
         }
         return hipGetLastError();
@@ -3163,17 +3224,17 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRaysShadow));
-        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
+        const dim3 bb(kBinBlock);
         const int mode = extend_mode();
         const PathQueue npq{nullptr, nullptr, nullptr, nullptr, nullptr};
         if (mode == 1 && bin_ok(S) && shadow_bin()) {
-            hipLaunchKernelGGL((k_trace_bin<true, false>), gb, bb, 0, st, S, npq, sq, shcnt, G, rec, nullptr);
+            hipLaunchKernelGGL((k_trace_bin<true, false>), (bin_grid<true, false>(G)), bb, 0, st, S, npq, sq, shcnt, G, rec, nullptr);
             return hipGetLastError();
         }
         if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK: the occlusion of both kernels, before the record update
             uint32_t *flags = reinterpret_cast<uint32_t *>(check_scratch((size_t)G * kSeg * sizeof(float4)));
             if (!flags) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL((k_trace_bin<true, true>), gb, bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
+            hipLaunchKernelGGL((k_trace_bin<true, true>), (bin_grid<true, true>(G)), bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
             hipLaunchKernelGGL(k_shadow_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, S, sq, shcnt, G, flags);
         }
         hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, b, 0, st, S, sq, shcnt, rec, G);
