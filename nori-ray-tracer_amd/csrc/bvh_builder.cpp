@@ -323,9 +323,7 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
         }
     }
     uint32_t n = (uint32_t)prim_shape.size();
-    const uint32_t width = out.width;  // the caller's choice survives the reset
     out = DeviceBvh();
-    out.width = width;
     if (n == 0) throw NoriException(NORI_ERR_INVALID, "scene has no primitives");
     if (n >= (1u << 25)) throw NoriException(NORI_ERR_UNSUPPORTED, "more than 2^25 primitives");
     auto T0 = std::chrono::steady_clock::now();
@@ -465,8 +463,7 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
     } else {
         emit(0, 0);
     }
-    // ---- collapse the binary device tree into the W-wide layout (W = 4 or 8)
-    const uint32_t W = out.width == 8 ? 8u : 4u, NF = 8 * W;  // floats per node: 6 W box planes, W refs, padding
+    // ---- collapse the binary device tree into the 4-wide layout
     std::vector<float> bin;
     bin.swap(nodes);
     struct C4 {
@@ -489,12 +486,12 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
         return 2.0f * ((d[0] * d[1] + d[1] * d[2]) + d[2] * d[0]);
     };
     auto empty = [](const C4 &c) { return c.mn[0] > c.mx[0] || c.mn[1] > c.mx[1] || c.mn[2] > c.mx[2]; };
-    uint32_t depthw = 0;
+    uint32_t depth4 = 0;
     std::function<uint32_t(uint32_t, uint32_t)> collapse = [&](uint32_t n, uint32_t depth) -> uint32_t {
         C4 two[2];
         kids(n, two);
         std::vector<C4> ch(two, two + 2);
-        while (ch.size() < W) {  // open the inner child of largest area (DFS order kept)
+        while (ch.size() < 4) {  // open the inner child of largest area (DFS order kept)
             int best = -1;
             float ba = -1.0f;
             for (size_t i = 0; i < ch.size(); ++i)
@@ -507,27 +504,26 @@ void build_device_bvh(const nori_scene_desc &d, const float root_min[3], const f
             ch[(size_t)best] = two[0];
             ch.insert(ch.begin() + best + 1, two[1]);
         }
-        const uint32_t me = (uint32_t)(nodes.size() / NF);
-        nodes.resize(nodes.size() + NF, 0.0f);
-        depthw = std::max(depthw, depth + 1);
-        uint32_t refs[8];
-        for (uint32_t i = 0; i < W; ++i) {
+        const uint32_t me = (uint32_t)(nodes.size() / 32);
+        nodes.resize(nodes.size() + 32, 0.0f);
+        depth4 = std::max(depth4, depth + 1);
+        uint32_t refs[4];
+        for (int i = 0; i < 4; ++i) {
             const bool use = (size_t)i < ch.size() && !empty(ch[(size_t)i]);
             refs[i] = use ? ch[(size_t)i].ref : kLeafBit;  // unused: NaN box, never entered
             if (use && !(refs[i] & kLeafBit)) refs[i] = collapse(refs[i], depth + 1);
-            float *nd = &nodes[NF * (size_t)me];
+            float *nd = &nodes[32 * (size_t)me];
             for (int k = 0; k < 3; ++k) {
-                nd[W * k + i] = use ? ch[(size_t)i].mn[k] : __builtin_nanf("");
-                nd[W * (3 + k) + i] = use ? ch[(size_t)i].mx[k] : __builtin_nanf("");
+                nd[4 * k + i] = use ? ch[(size_t)i].mn[k] : __builtin_nanf("");
+                nd[4 * (3 + k) + i] = use ? ch[(size_t)i].mx[k] : __builtin_nanf("");
             }
         }
-        std::memcpy(&nodes[NF * (size_t)me + 6 * W], refs, 4 * W);
+        std::memcpy(&nodes[32 * (size_t)me + 24], refs, 16);
         return me;
     };
     collapse(0, 0);
-    out.num_nodes = (uint32_t)(nodes.size() / NF);
-    out.depth = depthw;
-    out.width = W;
+    out.num_nodes = (uint32_t)(nodes.size() / 32);
+    out.depth = depth4;
     (void)max_depth;
     lap("device layout");
 }

@@ -75,11 +75,10 @@ int load_exr(const std::string &path, int &width, int &height, std::vector<float
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kLeafMaxPrims = 64;
 struct DeviceBvh {
-    std::vector<float> nodes;   // 8 W floats per W-wide node (32: 4-wide, 64: 8-wide)
+    std::vector<float> nodes;   // 32 floats per 4-wide node
     std::vector<float> prims;   // 12 floats per primitive
-    uint32_t width = 4;          // set before build_device_bvh: 4 or 8 children per node
     uint32_t num_nodes = 0;
-    uint32_t depth = 0;          // max inner-node depth of the W-wide tree (stack bound: W - 1 per level)
+    uint32_t depth = 0;          // max inner-node depth of the 4-wide tree (stack bound: 3 per level)
     uint32_t ref_nodes = 0;      // nodes of the reference-layout tree
     float sah_cost = 0;
 };

@@ -85,5 +85,6 @@ bool trav_stats_take(unsigned long long out[8]);  // NORI_TRAV_STATS builds (dia
 // both, compared (NORI_EXTEND_CHECK=1); extend_check_take reads and resets
 // (hit mismatches, compared extension rays, occlusion mismatches, compared shadow rays).
 int extend_mode();
+bool ext_prof_take(unsigned long long out[4]);  // NORI_PROF_EXTEND builds (diagnostic)
 bool extend_check_take(unsigned long long out[4]);
 }  // namespace nori

@@ -188,6 +188,9 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
     return (disc > 0) && (h1 || h2);
 }
 
+#ifndef NORI_CAMERA_CULL
+#define NORI_CAMERA_CULL 1
+#endif
 // Small scenes: wave-uniform scan of the primitive list.  Every lane tests
 // every primitive the wave needs in the same order, so the records arrive
 // through scalar loads and no lane diverges; the result is the closest hit.
@@ -242,6 +245,26 @@ ND bool plane_may_hit(float o, float d, float c, float mint, float maxt) {
     return s > lo && s < hi;
 }
 
+template <int A>
+ND float comp(const V3 &v) { return A == 0 ? v.x : A == 1 ? v.y : v.z; }
+
+// May the Moller-Trumbore test of a triangle of this pair accept the ray?
+// false is exact (runtime.hip plane_filters): the crossing t_f must lie in
+// [mint, maxt] up to the plane_may_hit margins (|t_f / t - 1| <= gamma_3 on
+// top of its 133 u), and its in-plane point within the widened rectangle.
+// NaN and infinite crossings (d_A = 0: det = 0, never accepted) fail the
+// range test or pass the rectangle test, never wrongly reject.
+template <int A>
+ND bool pair_candidate(const TRay &r, const float4 &f0, const float4 &f1, float mlo, float mhi, float so, float sd) {
+    constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+    const float tf = (f1.y - comp<A>(r.o)) * comp<A>(r.rcp);
+    const float dB = __builtin_fmaf(tf, comp<B>(r.d), comp<B>(r.o) - f0.x);
+    const float dC = __builtin_fmaf(tf, comp<C>(r.d), comp<C>(r.o) - f0.z);
+    const float S = __builtin_fmaf(fabsf(tf), sd, so);
+    const float thB = __builtin_fmaf(f1.x, S, f0.y), thC = __builtin_fmaf(f1.x, S, f0.w);
+    return tf > mlo && tf <= mhi && !(fabsf(dB) > thB) && !(fabsf(dC) > thC);
+}
+
 // One triangle record against K rays; the tie rule above.  PLANE 0-2: an
 // axis-plane triangle of that axis (tri_hit_plane), -1: any triangle.
 template <int K, bool ANY, int PLANE = -1>
@@ -275,12 +298,25 @@ ND void scan_tri(const float4 &a, const float4 &b, const float4 &c, TRay (&r)[K]
 // (measured: the checks cost 7 % of the kernel's instructions and skip almost
 // nothing), while shadow rays, short segments towards the lights, skip most
 // walls.
-template <int A, int K, bool ANY, bool CULL>
+template <int A, int K, bool ANY, int CULL, bool GEN = false>
 ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                     uint32_t (&lb)[K], float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
     const uint32_t g0 = A == 0 ? 0u : S.plane_end[A - 1], g1 = S.plane_end[A];
     for (uint32_t g = g0; g < g1; ++g) {
-        if (CULL) {
+        if (CULL == 2) {  // the in-plane filter (pair_candidate): the whole rectangle, not only the plane
+            constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
+            const float4 f0 = S.plane_f[2 * g], f1 = S.plane_f[2 * g + 1];
+            bool may = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const float mlo = r[k].mint > 0.0f ? r[k].mint * kPlaneLo : -INF_F;
+                const float mhi = r[k].maxt > 0.0f ? r[k].maxt * kPlaneHi : INF_F;
+                const float so = fabsf(comp<B>(r[k].o)) + fabsf(comp<C>(r[k].o));
+                const float sd = fabsf(comp<B>(r[k].d)) + fabsf(comp<C>(r[k].d));
+                may = may || (live[k] && pair_candidate<A>(r[k], f0, f1, mlo, mhi, so, sd));
+            }
+            if (!__any(may)) continue;
+        } else if (CULL) {
             const float c = S.plane_c[g];
             bool may = false;
 #pragma unroll
@@ -295,12 +331,16 @@ ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], floa
         float4 q[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) q[j] = p[j];
-        scan_tri<K, ANY, A>(q[0], q[1], q[2], r, live, tb, pb, lb, ub, vb, found);
-        scan_tri<K, ANY, A>(q[3], q[4], q[5], r, live, tb, pb, lb, ub, vb, found);
+        scan_tri<K, ANY, GEN ? -1 : A>(q[0], q[1], q[2], r, live, tb, pb, lb, ub, vb, found);
+        scan_tri<K, ANY, GEN ? -1 : A>(q[3], q[4], q[5], r, live, tb, pb, lb, ub, vb, found);
     }
 }
 
-template <int K, bool ANY, bool CULL>
+// ZMINT (the trace API, whose rays may carry mint <= 0): a wave holding such
+// a ray tests the pairs with the generic test -- tri_hit_plane returns the
+// same t except for the sign of an exactly zero t, which only mint <= 0 can
+// accept.
+template <int K, bool ANY, int CULL, bool ZMINT = false>
 ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                   float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
     scan_prologue<K>(S, r, live);
@@ -319,10 +359,21 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
         for (int k = 0; k < K; ++k) done = done && (found[k] || !live[k]);
         return __all(done);
     };
-    if (S.plane_end[2]) {
+    bool gen = false;
+    if constexpr (ZMINT) {
+        bool z = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) z = z || (live[k] && !(r[k].mint > 0.0f));
+        gen = __any(z);
+    }
+    if (S.plane_end[2] && !gen) {
         scan_planes<0, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<1, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<2, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
+    } else if (ZMINT && S.plane_end[2]) {
+        scan_planes<0, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<1, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<2, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
     }
     const uint32_t nt = S.num_scan_tris, n = S.num_prims, real = S.num_scan_real;
     for (uint32_t i = 2 * S.plane_end[2]; i < nt; i += kScanGroup) {
@@ -363,10 +414,10 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
 // gives the VALU K independent dependency chains to interleave.  Results are
 // those of traverse<0, ANY> ray by ray.  CULL: the wave-wide plane skips
 // (every caller but the extension kernel, whose waves are incoherent).
-template <int K, bool ANY, bool CULL = true>
+template <int K, bool ANY, int CULL = 1, bool ZMINT = false>
 ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                   float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
-    scan_core<K, ANY, CULL>(S, r, live, tb, pb, ub, vb, found);
+    scan_core<K, ANY, CULL, ZMINT>(S, r, live, tb, pb, ub, vb, found);
 }
 
 // Primitive records fetched per memory round trip in a BVH leaf.
@@ -390,8 +441,7 @@ static __device__ unsigned long long g_trav_stats[8];
 // LDS words per lane of a traversal stack of depth STACK: child refs and entry distances.
 // (stack_lds_entries(STACK) entries: the LDS budget stays STACK words, so the
 // occupancy does not change; deeper entries spill to private memory)
-// (odd STACK: the 8-wide tree, STACK & ~1 LDS words per lane)
-constexpr int stack_words(int STACK) { return STACK ? (STACK & ~1) : 1; }
+constexpr int stack_words(int STACK) { return STACK ? STACK : 1; }
 
 // BVH::rayIntersect (bvh.cpp:404-462): adaptive epsilon, closest or any hit.
 // Near child first; the short stack lives in LDS, one column per lane.
@@ -458,54 +508,7 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     } flush{tstat};
 #endif
     for (;;) {
-        if (!(ref & 0x80000000u) && (STACK & 1)) {
-            // 8-wide node (odd STACK): 16 float4 = 256 B, the child boxes
-            // in SoA form (min.x of children 0-3 | 4-7, min.y, ..., max.z),
-            // the refs of children 0-3 | 4-7, padding.  The hit children are
-            // ordered by entry distance with Batcher's 19-comparator network on
-            // (sortable key bits, ref); misses carry the largest key and sort last.
-            NORI_TSTAT(0, 1);
-            const float4 *nd = S.nodes + 16 * (size_t)ref;
-            float4 v[14];
-#pragma unroll
-            for (int j = 0; j < 14; ++j) v[j] = gld(nd + j);
-            uint32_t kk[8], cc[8];
-            int nh = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int h = i >> 2, e = i & 3;
-                auto el = [e](const float4 &f) { return e == 0 ? f.x : e == 1 ? f.y : e == 2 ? f.z : f.w; };
-                float k;
-                const bool hit = box_test(make_float4(el(v[h]), el(v[2 + h]), el(v[4 + h]), 0),
-                                          make_float4(el(v[6 + h]), el(v[8 + h]), el(v[10 + h]), 0), r, k);
-                const uint32_t kb = __float_as_uint(k);
-                kk[i] = hit ? ((kb & 0x80000000u) ? ~kb : (kb | 0x80000000u)) : 0xFFFFFFFFu;
-                cc[i] = __float_as_uint(el(v[12 + h]));
-                nh += hit ? 1 : 0;
-            }
-            if (nh > 0) {
-                auto cs = [&](int a, int b) {
-                    const bool sw = kk[b] < kk[a];
-                    const uint32_t ka = kk[a], ca = cc[a];
-                    kk[a] = sw ? kk[b] : ka;
-                    kk[b] = sw ? ka : kk[b];
-                    cc[a] = sw ? cc[b] : ca;
-                    cc[b] = sw ? ca : cc[b];
-                };
-                cs(0, 1); cs(2, 3); cs(4, 5); cs(6, 7);
-                cs(0, 2); cs(1, 3); cs(4, 6); cs(5, 7);
-                cs(1, 2); cs(5, 6);
-                cs(0, 4); cs(1, 5); cs(2, 6); cs(3, 7);
-                cs(2, 4); cs(3, 5);
-                cs(1, 2); cs(3, 4); cs(5, 6);
-                auto unkey = [](uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); };
-#pragma unroll
-                for (int i = 7; i >= 1; --i)
-                    if (i < nh) push(sp, cc[i], unkey(kk[i]));
-                ref = cc[0];
-                continue;
-            }
-        } else if (!(ref & 0x80000000u)) {
+        if (!(ref & 0x80000000u)) {
             NORI_TSTAT(0, 1);
             float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
             load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
@@ -625,7 +628,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 
     r.maxt = b.w;
     float t, u, v;
     uint32_t p;
-    bool h = traverse<STACK, ANY>(S, r, stk + threadIdx.x, t, p, u, v);
+    bool h;
+    if constexpr (STACK == 0) {  // the caller's rays: mint may be <= 0 (scan_core ZMINT)
+        TRay rr[1] = {r};
+        bool live[1] = {true}, found[1];
+        float t1[1], u1[1], v1[1];
+        uint32_t p1[1];
+        scan_rays<1, ANY, 1, true>(S, rr, live, t1, p1, u1, v1, found);
+        t = t1[0], p = p1[0], u = u1[0], v = v1[0], h = found[0];
+    } else {
+        h = traverse<STACK, ANY>(S, r, stk + threadIdx.x, t, p, u, v);
+    }
     if (ANY) hits[q] = make_float4(h ? 0.0f : INF_F, __uint_as_float(h ? 0u : 0xFFFFFFFFu), 0.0f, 0.0f);
     else hits[q] = make_float4(t, __uint_as_float(p), u, v);
 }
@@ -759,10 +772,16 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
+#ifdef NORI_PROF_EXTEND
+static __device__ unsigned long long g_ext_prof[4];  // per wave: loads, scan, store clocks; waves
+#endif
 template <int K>
 __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
                                                              uint32_t G) {
     const SegRange sr = seg_range_k(cnt, G, K);
+    // a lane's K rays are entries kTraceBlock apart (adjacent entries, so
+    // that a wave covers 64 K consecutive ones, measured 1 % slower)
+    constexpr uint32_t STEP = kTraceBlock;
     const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
     if (i0 >= n) return;  // entries fill the slice from its start
     TRay r[K];
@@ -770,20 +789,54 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQue
     uint32_t q[K];
     // lanes past the end load entry i0 again (unconditional loads: no
     // branch, so all of them are in flight together)
+#ifdef NORI_PROF_EXTEND  // diagnostic build: shader clocks of the wave's phases (ext_prof_take)
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
+    bool cam = true;  // every live ray of this lane a camera ray
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint32_t i = i0 + k * kTraceBlock;
+        const uint32_t i = i0 + k * STEP;
         live[k] = i < n;
         q[k] = seg_entry(sr, live[k] ? i : i0);
-        path_ray(S, pq.ray_o[q[k]], pq.ray_d[q[k]], r[k]);
+        const float4 b = pq.ray_d[q[k]];
+        path_ray(S, pq.ray_o[q[k]], b, r[k]);
+        cam = cam && (!live[k] || (__float_as_uint(b.w) & kCameraRay) != 0u);
     }
     float t[K], u[K], v[K];
     uint32_t p[K];
     bool f[K];
-    scan_rays<K, false, false>(S, r, live, t, p, u, v, f);
+    // A wave of camera rays (the tail of a segment: new samples, adjacent
+    // pixels) is coherent: its rays leave through one or two walls, so the
+    // in-plane filter skips the other pairs for the whole wave.  The
+    // incoherent waves of bounce rays test every pair unchecked (a wave-wide
+    // skip never happens there; NORI_CAMERA_CULL=0 tests every wave so).
+#ifdef NORI_PROF_EXTEND
+    {  // wait for the ray loads: the first use of every loaded word
+        float z = 0.0f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) z += r[k].o.x + r[k].o.y + r[k].o.z + r[k].d.x + r[k].d.y + r[k].d.z + r[k].mint;
+        if (__builtin_isnan(z) && threadIdx.x == 1000) r[0].mint = z;
+    }
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
+    if (NORI_CAMERA_CULL && S.plane_f && __all(cam)) scan_rays<K, false, 2>(S, r, live, t, p, u, v, f);
+    else scan_rays<K, false, 0>(S, r, live, t, p, u, v, f);
+#ifdef NORI_PROF_EXTEND
+    const uint64_t c2 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        if (i0 + k * kTraceBlock < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
+        if (i0 + k * STEP < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
+#ifdef NORI_PROF_EXTEND
+    __builtin_amdgcn_s_waitcnt(0);  // the stores' completion
+    const uint64_t c3 = __builtin_amdgcn_s_memtime();
+    if (lane_id() == 0) {
+        atomicAdd(&g_ext_prof[0], (unsigned long long)(c1 - c0));
+        atomicAdd(&g_ext_prof[1], (unsigned long long)(c2 - c1));
+        atomicAdd(&g_ext_prof[2], (unsigned long long)(c3 - c2));
+        atomicAdd(&g_ext_prof[3], 1ull);
+    }
+#endif
 }
 
 template <int K>
@@ -840,7 +893,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
 // launch).  A ray with more than kBinSlots candidates tests everything in its
 // own lane.
 #ifndef NORI_EXTEND_BIN
-#define NORI_EXTEND_BIN 1
+#define NORI_EXTEND_BIN 0
 #endif
 #ifndef NORI_BIN_SPHERES
 #define NORI_BIN_SPHERES 1
@@ -852,26 +905,6 @@ constexpr int kBinBlock = 256;
 constexpr uint32_t kBinSlices = kTraceGroup * kSeg / kBinBlock;  // work-groups per group of segments
 constexpr int kBinSlots = 3;
 constexpr uint32_t kBinMaxRec = 64;  // staged records: the pairs' (2 per pair) and the spheres'
-template <int A>
-ND float comp(const V3 &v) { return A == 0 ? v.x : A == 1 ? v.y : v.z; }
-
-// May the Moller-Trumbore test of a triangle of this pair accept the ray?
-// false is exact (runtime.hip plane_filters): the crossing t_f must lie in
-// [mint, maxt] up to the plane_may_hit margins (|t_f / t - 1| <= gamma_3 on
-// top of its 133 u), and its in-plane point within the widened rectangle.
-// NaN and infinite crossings (d_A = 0: det = 0, never accepted) fail the
-// range test or pass the rectangle test, never wrongly reject.
-template <int A>
-ND bool pair_candidate(const TRay &r, const float4 &f0, const float4 &f1, float mlo, float mhi, float so, float sd) {
-    constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
-    const float tf = (f1.y - comp<A>(r.o)) * comp<A>(r.rcp);
-    const float dB = __builtin_fmaf(tf, comp<B>(r.d), comp<B>(r.o) - f0.x);
-    const float dC = __builtin_fmaf(tf, comp<C>(r.d), comp<C>(r.o) - f0.z);
-    const float S = __builtin_fmaf(fabsf(tf), sd, so);
-    const float thB = __builtin_fmaf(f1.x, S, f0.y), thC = __builtin_fmaf(f1.x, S, f0.w);
-    return tf > mlo && tf <= mhi && !(fabsf(dB) > thB) && !(fabsf(dC) > thC);
-}
-
 // A ray's candidates: count and up to kBinSlots entries of 8 bits (kind << 7
 // | index: kind 0 a pair, 1 a sphere), 8 bits apart.
 struct BinCand {
@@ -918,66 +951,27 @@ __global__ __launch_bounds__(kBinBlock) void k_trace_bin(DevScene S, PathQueue p
     __shared__ uint16_t s_item[2][NW][CAP];             // per kind and wave: ray | index << 8 | slot << 14
     __shared__ uint32_t s_nitem[2][NW];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const SegRange sr = seg_range_k(cnt, G, kTraceSlices / kBinSlices);
+    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % kBinSlices) * kBinBlock, i = i0 + tid;
+    if (i0 >= n) return;  // the whole work-group: its slice is empty
     const uint32_t np = S.plane_end[2], nt = S.num_scan_tris, nall = S.num_prims;
     const uint32_t ns = NORI_BIN_SPHERES ? nall - nt : 0u, sph0 = 6 * np;
     for (uint32_t j = tid; j < 6 * np; j += kBinBlock) s_rec[j] = S.prims[j];
     for (uint32_t j = tid; j < 3 * ns; j += kBinBlock) s_rec[sph0 + j] = S.prims[3 * nt + j];
-    // The work-groups stride over the slices (256 queue entries of a group of
-    // segments): a grid of resident work-groups loops, and the next slice's
-    // rays are loaded while this one is tested, so the ray loads' latency
-    // hides behind the tests (a grid of one work-group per slice runs each
-    // body once).
-    const uint32_t nsl = (G + kTraceGroup - 1) / kTraceGroup * kBinSlices;
-    struct Fetch {
-        uint32_t n, i0, q;
-        float4 a, b, c;
-    };
-    auto fetch = [&](uint32_t sl) {
-        Fetch f;
-        f.n = 0;
-        f.i0 = 0;
-        f.q = 0;
-        if (sl >= nsl) return f;
-        SegRange sr;
-        sr.s0 = (sl / kBinSlices) * kTraceGroup;
-        sr.pre[0] = 0;
-#pragma unroll
-        for (int k = 0; k < kTraceGroup; ++k) sr.pre[k + 1] = sr.pre[k] + (sr.s0 + k < G ? cnt[sr.s0 + k] : 0u);
-        f.n = sr.pre[kTraceGroup];
-        f.i0 = (sl % kBinSlices) * kBinBlock;
-        if (f.i0 >= f.n) return f;  // an empty slice
-        const uint32_t i = f.i0 + tid;
-        f.q = seg_entry(sr, i < f.n ? i : f.i0);
-        if constexpr (ANY) {
-            f.a = sq.ray_o[f.q];
-            f.b = sq.ray_d[f.q];
-            if (!FLAGS) f.c = sq.payload[f.q];
-        } else {
-            f.a = pq.ray_o[f.q];
-            f.b = pq.ray_d[f.q];
-        }
-        return f;
-    };
-    Fetch cur = fetch(blockIdx.x);
-    for (uint32_t sl = blockIdx.x; sl < nsl; sl += gridDim.x) {
-    const Fetch nxt = fetch(sl + gridDim.x);
-    if (cur.i0 >= cur.n) {  // (uniform) nothing queued in this slice
-        cur = nxt;
-        continue;
-    }
-    const uint32_t n = cur.n, i = cur.i0 + tid, q = cur.q;
     const bool valid = i < n;
+    const uint32_t q = seg_entry(sr, valid ? i : i0);
     TRay r[1];
     bool live[1] = {valid};
     float4 pay = make_float4(0, 0, 0, 0);
     if constexpr (ANY) {
-        if (!FLAGS) pay = cur.c;
-        r[0].o = ld3(cur.a);
-        r[0].d = ld3(cur.b);
-        r[0].mint = cur.a.w;
-        r[0].maxt = cur.b.w;
+        const float4 a = sq.ray_o[q], b = sq.ray_d[q];
+        if (!FLAGS) pay = sq.payload[q];  // fetched now: its latency hides behind the tests
+        r[0].o = ld3(a);
+        r[0].d = ld3(b);
+        r[0].mint = a.w;
+        r[0].maxt = b.w;
     } else {
-        path_ray(S, cur.a, cur.b, r[0]);
+        path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
     }
     scan_prologue<1>(S, r, live);
     float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
@@ -1128,14 +1122,10 @@ __global__ __launch_bounds__(kBinBlock) void k_trace_bin(DevScene S, PathQueue p
             }
         }
     }
-    if (valid) {
-        if constexpr (!ANY) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
-        else if constexpr (FLAGS) flags[q] = found[0] ? 1u : 0u;
-        else if (!found[0]) shadow_add(rec, pay);
-    }
-    __syncthreads();  // the LDS lists and results are reused by the next slice
-    cur = nxt;
-    }
+    if (!valid) return;
+    if constexpr (!ANY) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
+    else if constexpr (FLAGS) flags[q] = found[0] ? 1u : 0u;
+    else if (!found[0]) shadow_add(rec, pay);
 }
 
 // NORI_EXTEND_CHECK (diagnostic): mismatching hit records between the two
@@ -2788,7 +2778,6 @@ static void photons_dispatch(const DevScene &S, uint64_t e0, uint32_t n, uint32_
     case 0: hipLaunchKernelGGL((k_photons<0, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     case 8: hipLaunchKernelGGL((k_photons<8, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     case 16: hipLaunchKernelGGL((k_photons<16, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
-    case 17: hipLaunchKernelGGL((k_photons<17, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     default: hipLaunchKernelGGL((k_photons<32, STORE>), g, b, 0, st, S, e0, n, count, pre, total, out); break;
     }
 }
@@ -2802,12 +2791,6 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 
 #endif
 // ------------------------------------------------------------------ film splat
-#ifndef NORI_SPLAT2
-#define NORI_SPLAT2 0
-#endif
-#ifndef NORI_SPLAT2_WAVES
-#define NORI_SPLAT2_WAVES 4  // k_splat2: at most 128 VGPRs
-#endif
 #ifndef NORI_SPLAT_DEPTH
 #define NORI_SPLAT_DEPTH 1  // sample records in flight per thread (prefetch depth)
 #endif
@@ -2938,149 +2921,6 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
     }
 }
 
-// k_splat with a pixel's window split over two lanes by channel (NORI_SPLAT2):
-// lane 2i accumulates R and G, lane 2i+1 B and W of the same pixel, so each
-// holds 5 x 5 x 2 sums instead of 5 x 5 x 4 (k_splat's 256 VGPRs allow one
-// wave per SIMD, issuing at half rate with every latency exposed).  The pass
-// loop takes the pixel's samples two at a time: each lane regenerates the
-// jitter and the filter weights of one of them (lane parity = which) and the
-// pair swaps weights with one DPP move per value, so the per-sample work is
-// not doubled.  Every product and sum is the one k_splat computes, in the
-// same order per cell: ((L_c * wx) * wy) added pass by pass.
-ND float pair_swap(float v) {  // the partner lane's value (lanes 2i <-> 2i+1): DPP quad_perm [1, 0, 3, 2]
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-template <int B>
-__global__ __launch_bounds__(kSplatBlock) __attribute__((amdgpu_waves_per_eu(B <= 2 ? NORI_SPLAT2_WAVES : 1))) void k_splat2(DevScene S, const float4 *rec, SplatDesc sd, float *film,
-                                                       Counters *C) {
-    constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1;
-    __shared__ float tile[TS * TS * 4];
-    __shared__ float ftab[NORI_FILTER_RESOLUTION + 1];
-    int4 bi = sd.blocks[blockIdx.x];
-    const int ox = bi.x, oy = bi.y, bw = bi.z & 0xFFFF, bh = bi.z >> 16;
-    const uint32_t off = (uint32_t)bi.w;
-    const uint32_t p0 = blockIdx.y * sd.passes_per_wg, p1 = min(sd.passes, p0 + sd.passes_per_wg);
-    for (int i = threadIdx.x; i < TS * TS * 4; i += kSplatBlock) tile[i] = 0.0f;
-    if (threadIdx.x <= NORI_FILTER_RESOLUTION) ftab[threadIdx.x] = S.filter[threadIdx.x];
-    __syncthreads();
-    const int npix = bw * bh;
-    const float rad = S.filter_radius, lk = S.lookup;
-    const uint64_t WH = (uint64_t)S.W * (uint64_t)S.H;
-    const uint32_t ch = threadIdx.x & 1u;  // 0: R, G   1: B, W
-    uint32_t inval = 0;
-    // pixel rounds: the whole block iterates together so the DPP partners stay converged
-    for (int j0 = 0; j0 < npix; j0 += kSplatBlock / 2) {
-        const int j = j0 + (int)(threadIdx.x >> 1);
-        const bool pix = j < npix;
-        const int jj = pix ? j : 0;
-        const int ly = jj / bw, lx = jj - ly * bw, x = ox + lx, y = oy + ly;
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 acc[K][K];
-#pragma unroll
-        for (int a = 0; a < K; ++a)
-#pragma unroll
-            for (int c = 0; c < K; ++c) acc[a][c] = f2{0.0f, 0.0f};
-        bool any = false;
-        float vs[7] = {0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t p = p0; p < p1; p += 2) {
-            // the two samples of this pass pair, and this lane's one of them
-            float4 Ls[2];
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-                Ls[s] = pix && p + s < p1 ? rec[(size_t)(p + s) * sd.M + off + jj] : make_float4(0, 0, 0, 1);
-            const float4 L = ch ? Ls[1] : Ls[0];
-            bool use = L.w == 0.0f;  // not pending (the finisher splats pending samples)
-            const bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
-            if (use && !valid) ++inval;
-            use = use && valid;
-            float wx[K], wy[K];
-            {
-                uint64_t sid = (uint64_t)(sd.pass_begin + p + ch) * WH + (uint64_t)y * S.W + x;
-                Pcg r;
-                wave_seed(r, sd.seed, sid);
-                V2 jit = next2D(r);
-                float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
-                int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
-                int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
-#pragma unroll
-                for (int d = 0; d < K; ++d) {
-                    int cx = lx + d, cy = ly + d;
-                    int kx = min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION);
-                    int ky = min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION);
-                    const float fx = ftab[kx], fy = ftab[ky];
-                    wx[d] = (cx >= x0 && cx <= x1) ? fx : 0.0f;
-                    wy[d] = (cy >= y0 && cy <= y1) ? fy : 0.0f;
-                }
-            }
-            // the partner's weights and flag: sample 1 - ch
-            float ox_[K], oy_[K];
-#pragma unroll
-            for (int d = 0; d < K; ++d) {
-                ox_[d] = pair_swap(wx[d]);
-                oy_[d] = pair_swap(wy[d]);
-            }
-            const bool ouse = pair_swap(use ? 1.0f : 0.0f) != 0.0f;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const bool u = s == (int)ch ? use : ouse;
-                if (!u) continue;
-                const float4 Lq = Ls[s];
-                any = true;
-                if (ch == 0) {
-                    vs[0] += Lq.x;
-                    vs[1] += Lq.y;
-                    vs[2] += Lq.z;
-                    vs[3] += Lq.x * Lq.x;
-                    vs[4] += Lq.y * Lq.y;
-                    vs[5] += Lq.z * Lq.z;
-                    vs[6] += 1.0f;
-                }
-                const f2 Lc = ch ? f2{Lq.z, 1.0f} : f2{Lq.x, Lq.y};
-                f2 lw[K];
-#pragma unroll
-                for (int c = 0; c < K; ++c) lw[c] = Lc * (s == (int)ch ? wx[c] : ox_[c]);
-#pragma unroll
-                for (int a = 0; a < K; ++a) {
-                    const float wa = s == (int)ch ? wy[a] : oy_[a];
-#pragma unroll
-                    for (int c = 0; c < K; ++c) acc[a][c] += lw[c] * wa;
-                }
-            }
-        }
-        if (any && pix && ch == 0 && sd.var) {
-            float *v = sd.var + 8 * ((size_t)y * S.W + x);
-            for (int k = 0; k < 7; ++k) atomicAdd(v + k, vs[k]);
-        }
-        if (any && pix) {
-#pragma unroll
-            for (int a = 0; a < K; ++a)
-#pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    float *t = tile + 4 * ((ly + a) * TS + (lx + c)) + 2 * ch;
-                    const f2 v = acc[a][c];
-                    if (v.x != 0.0f || v.y != 0.0f) {
-                        atomicAdd(t + 0, v.x);
-                        atomicAdd(t + 1, v.y);
-                    }
-                }
-        }
-    }
-    if (inval) atomicAdd(&C->invalid, (unsigned long long)inval);
-    __syncthreads();
-    const int rows = bh + 2 * B, cols = bw + 2 * B, FW = S.W + 2 * B;
-    for (int i = threadIdx.x; i < rows * cols; i += kSplatBlock) {
-        int yy = i / cols, xx = i - yy * cols;
-        const float *c = tile + 4 * (yy * TS + xx);
-        float *f = film + 4 * ((size_t)(oy + yy) * FW + (ox + xx));
-        if (c[3] != 0.0f || c[0] != 0.0f || c[1] != 0.0f || c[2] != 0.0f) {
-            atomicAdd(f + 0, c[0]);
-            atomicAdd(f + 1, c[1]);
-            atomicAdd(f + 2, c[2]);
-            atomicAdd(f + 3, c[3]);
-        }
-    }
-}
-
 // ------------------------------------------------------------------ launchers
 #if NORI_TU == 0
 template <bool ANY>
@@ -3091,7 +2931,6 @@ static hipError_t trace_dispatch(const DevScene &S, const float4 *rays, uint32_t
     case 0: hipLaunchKernelGGL((k_trace<0, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 8: hipLaunchKernelGGL((k_trace<8, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 16: hipLaunchKernelGGL((k_trace<16, ANY>), g, b, 0, st, S, rays, n, hits); break;
-    case 17: hipLaunchKernelGGL((k_trace<17, ANY>), g, b, 0, st, S, rays, n, hits); break;
     case 32: hipLaunchKernelGGL((k_trace<32, ANY>), g, b, 0, st, S, rays, n, hits); break;
     default: hipLaunchKernelGGL((k_trace<64, ANY>), g, b, 0, st, S, rays, n, hits); break;
     }
@@ -3155,24 +2994,6 @@ static bool shadow_bin() {
     }();
     return on;
 }
-// Grid of a binned trace launch: the resident work-groups (occupancy x CUs,
-// queried once per kernel), which loop over the slices prefetching the next
-// one's rays; NORI_BIN_PERSIST=0: one work-group per slice.
-template <bool ANY, bool FLAGS>
-static dim3 bin_grid(uint32_t G) {
-    const uint32_t nsl = (G + kTraceGroup - 1) / kTraceGroup * kBinSlices;
-    static const uint32_t resident = [] {
-        const char *e = std::getenv("NORI_BIN_PERSIST");
-        if (e && e[0] == '0') return 0u;
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trace_bin<ANY, FLAGS>, kBinBlock, 0) != hipSuccess)
-            return 0u;
-        return (uint32_t)(cus * per);
-    }();
-    return dim3(resident ? std::min(nsl, resident) : nsl);
-}
 // Diagnostic scratch of NORI_EXTEND_CHECK (grown as needed, never freed).
 static float4 *check_scratch(size_t bytes) {
     static float4 *p = nullptr;
@@ -3191,11 +3012,11 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
-        const dim3 bb(kBinBlock);
+        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
         const int mode = extend_mode();
         const ShadowQueue nsq{nullptr, nullptr, nullptr};
         if (mode == 1 && bin_ok(S)) {
-            hipLaunchKernelGGL((k_trace_bin<false, false>), (bin_grid<false, false>(G)), bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
+            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
             return hipGetLastError();
         }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
@@ -3204,7 +3025,7 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
             if (!scratch) return hipErrorOutOfMemory;
             PathQueue q2 = q;
             q2.hit = scratch;
-            hipLaunchKernelGGL((k_trace_bin<false, false>), (bin_grid<false, false>(G)), bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
+            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
             hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
         }
         return hipGetLastError();
@@ -3212,7 +3033,6 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
     switch (stack) {
     case 8: hipLaunchKernelGGL(k_extend<8>, g, b, 0, st, S, q, cnt, G); break;
     case 16: hipLaunchKernelGGL(k_extend<16>, g, b, 0, st, S, q, cnt, G); break;
-    case 17: hipLaunchKernelGGL(k_extend<17>, g, b, 0, st, S, q, cnt, G); break;
     case 32: hipLaunchKernelGGL(k_extend<32>, g, b, 0, st, S, q, cnt, G); break;
     default: hipLaunchKernelGGL(k_extend<64>, g, b, 0, st, S, q, cnt, G); break;
     }
@@ -3224,17 +3044,17 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
         dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRaysShadow));
-        const dim3 bb(kBinBlock);
+        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
         const int mode = extend_mode();
         const PathQueue npq{nullptr, nullptr, nullptr, nullptr, nullptr};
         if (mode == 1 && bin_ok(S) && shadow_bin()) {
-            hipLaunchKernelGGL((k_trace_bin<true, false>), (bin_grid<true, false>(G)), bb, 0, st, S, npq, sq, shcnt, G, rec, nullptr);
+            hipLaunchKernelGGL((k_trace_bin<true, false>), gb, bb, 0, st, S, npq, sq, shcnt, G, rec, nullptr);
             return hipGetLastError();
         }
         if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK: the occlusion of both kernels, before the record update
             uint32_t *flags = reinterpret_cast<uint32_t *>(check_scratch((size_t)G * kSeg * sizeof(float4)));
             if (!flags) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL((k_trace_bin<true, true>), (bin_grid<true, true>(G)), bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
+            hipLaunchKernelGGL((k_trace_bin<true, true>), gb, bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
             hipLaunchKernelGGL(k_shadow_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, S, sq, shcnt, G, flags);
         }
         hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, b, 0, st, S, sq, shcnt, rec, G);
@@ -3243,7 +3063,6 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
     switch (stack) {
     case 8: hipLaunchKernelGGL(k_shadow<8>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 16: hipLaunchKernelGGL(k_shadow<16>, g, b, 0, st, S, sq, shcnt, rec, G); break;
-    case 17: hipLaunchKernelGGL(k_shadow<17>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     case 32: hipLaunchKernelGGL(k_shadow<32>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     default: hipLaunchKernelGGL(k_shadow<64>, g, b, 0, st, S, sq, shcnt, rec, G); break;
     }
@@ -3295,7 +3114,6 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
         break;
     case 8: hipLaunchKernelGGL((k_finish<8, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     case 16: hipLaunchKernelGGL((k_finish<16, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
-    case 17: hipLaunchKernelGGL((k_finish<17, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     case 32: hipLaunchKernelGGL((k_finish<32, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     default: hipLaunchKernelGGL((k_finish<64, INTEG, false, VAR>), g, b, 0, st, S, Q, seg, sel, rec, wd, film, C, pre, G); break;
     }
@@ -3330,7 +3148,6 @@ static void direct_dispatch(const DevScene &S, const WorkDesc &wd, float4 *rec, 
     case 0: hipLaunchKernelGGL((k_direct<0, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     case 8: hipLaunchKernelGGL((k_direct<8, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     case 16: hipLaunchKernelGGL((k_direct<16, INTEG>), g, b, 0, st, S, wd, rec, C); break;
-    case 17: hipLaunchKernelGGL((k_direct<17, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     default: hipLaunchKernelGGL((k_direct<32, INTEG>), g, b, 0, st, S, wd, rec, C); break;
     }
 }
@@ -3369,6 +3186,17 @@ bool extend_check_take(unsigned long long out[4]) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_extend_check), z, sizeof(z)) == hipSuccess;
 }
 
+// NORI_PROF_EXTEND builds: read (and reset) k_extend_scan's phase clocks; false otherwise.
+bool ext_prof_take(unsigned long long out[4]) {
+#ifdef NORI_PROF_EXTEND
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ext_prof), 4 * sizeof(unsigned long long)) != hipSuccess) return false;
+    unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ext_prof), z, sizeof(z)) == hipSuccess;
+#else
+    (void)out;
+    return false;
+#endif
+}
 // NORI_TRAV_STATS builds: read (and reset) the BVH walk counters; false otherwise.
 bool trav_stats_take(unsigned long long out[8]) {
 #ifdef NORI_TRAV_STATS
@@ -3386,21 +3214,6 @@ hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &s
                         Counters *C, hipStream_t st) {
     if (nblocks == 0 || sd.passes == 0) return hipSuccess;
     dim3 g(nblocks, (sd.passes + sd.passes_per_wg - 1) / sd.passes_per_wg), b(kSplatBlock);
-    static const bool two = [] {
-        const char *e = std::getenv("NORI_SPLAT2");
-        return e ? e[0] == '1' : NORI_SPLAT2 != 0;
-    }();
-    if (two) {
-        switch (S.border) {
-        case 0: hipLaunchKernelGGL(k_splat2<0>, g, b, 0, st, S, rec, sd, film, C); break;
-        case 1: hipLaunchKernelGGL(k_splat2<1>, g, b, 0, st, S, rec, sd, film, C); break;
-        case 2: hipLaunchKernelGGL(k_splat2<2>, g, b, 0, st, S, rec, sd, film, C); break;
-        case 3: hipLaunchKernelGGL(k_splat2<3>, g, b, 0, st, S, rec, sd, film, C); break;
-        case 4: hipLaunchKernelGGL(k_splat2<4>, g, b, 0, st, S, rec, sd, film, C); break;
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
     switch (S.border) {
     case 0: hipLaunchKernelGGL(k_splat<0>, g, b, 0, st, S, rec, sd, film, C); break;
     case 1: hipLaunchKernelGGL(k_splat<1>, g, b, 0, st, S, rec, sd, film, C); break;

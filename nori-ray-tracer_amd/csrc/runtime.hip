@@ -779,16 +779,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     bool scan = off <= kScanMaxPrims;
     if (mode && std::string(mode) == "bvh") scan = false;
     if (mode && std::string(mode) == "scan") scan = true;
-    // BVH width: 4 children per node, or 8 (NORI_BVH_WIDTH=8): the same
-    // candidate primitives (box tests are monotone), fewer, wider steps.
     DeviceBvh bvh;
-    if (const char *e = std::getenv("NORI_BVH_WIDTH"); e && std::atoi(e) == 8 && !scan) bvh.width = 8;
     build_device_bvh(d, rmin, rmax, bvh);
     c.bvh_depth = bvh.depth;
     c.bvh_nodes = bvh.num_nodes;
-    // traversal stack: at most W - 1 entries per level of the W-wide tree;
-    // the first `stack` live in LDS, up to kTraceSpill more in private memory
-    const uint32_t need = (bvh.width - 1) * bvh.depth + 1;
+    // traversal stack: at most 3 entries per level of the 4-wide tree; the
+    // first `stack` live in LDS, up to kTraceSpill more in private memory
+    // (an 8-wide tree, 256-B nodes with a 19-comparator child order, was
+    // measured 15 % slower on C3 in round 5: DESIGN.md section 5)
+    const uint32_t need = 3 * bvh.depth + 1;
     // (LDS budget 16 words: measured best on the 22.7k and 524k triangle
     // scenes -- occupancy beats a deeper LDS part; 32 only when the spill
     // area could not cover the rest)
@@ -799,12 +798,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         const int v = std::atoi(e);
         if (v == 8 || v == 16 || v == 32) c.stack = v;
     }
-    if (bvh.width == 8) {  // the 8-wide kernels exist for a 16-word LDS stack only (c.stack = 16 | 1)
-        if (need > (uint32_t)stack_lds_entries(16) + kTraceSpill)
-            throw NoriException(NORI_ERR_UNSUPPORTED, "BVH too deep for the 8-wide traversal stack");
-        c.stack = 16 | 1;
-    }
-    if (need > (uint32_t)stack_lds_entries(c.stack & ~1) + kTraceSpill) throw NoriException(NORI_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
+    if (need > (uint32_t)stack_lds_entries(c.stack) + kTraceSpill) throw NoriException(NORI_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
     if (scan) c.stack = 0;
     ScanList scan_list;
     if (scan) scan_list = build_scan_list(bvh, off);
@@ -1467,6 +1461,10 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         }
         if (debug_log())
         {
+            unsigned long long ep[4];
+            if (ext_prof_take(ep) && ep[3])
+                std::fprintf(stderr, "[nori] k_extend_scan clocks per wave: loads + prologue %.0f, scan %.0f, stores %.0f (%llu waves)\n",
+                             (double)ep[0] / ep[3], (double)ep[1] / ep[3], (double)ep[2] / ep[3], ep[3]);
             unsigned long long ts[8];
             if (trav_stats_take(ts) && ts[3])
                 std::fprintf(stderr, "[nori] BVH walks: %llu rays, per ray %.2f inner nodes, %.2f leaves, %.2f primitives; "
