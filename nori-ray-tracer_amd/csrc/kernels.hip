@@ -191,6 +191,51 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
 #ifndef NORI_CAMERA_CULL
 #define NORI_CAMERA_CULL 1
 #endif
+// sphere_hit_nb with its square root and its two divisions in short
+// correctly rounded forms, so the same t bits for every ray: sqrt_rn's core
+// (v_sqrt_f32 and one Tuckerman test each way, exhaustively exact on
+// [2^-96, 2^96), device_math.h) and Markstein's quotient x / y =
+// fma(fma(-y, q0, x), r, q0), q0 = x r, r = 1/y correctly rounded (rcp_rn),
+// exact for |x|, |y| in [2^-60, 2^60] (tools/div_check.c: 8.2e8 quotients,
+// no mismatch).  Rays with disc > 0 outside those ranges take the IEEE
+// forms; rays with disc <= 0 miss either way.
+#ifndef NORI_SPHERE_FAST
+#define NORI_SPHERE_FAST 1
+#endif
+ND bool in_range60(float x) { return fabsf(x) >= 0x1p-60f && fabsf(x) <= 0x1p60f; }
+ND bool sphere_hit_fast(const float4 &a, const float4 &b, const TRay &r, float &t) {
+    if (!NORI_SPHERE_FAST) return sphere_hit_nb(a, b, r, t);
+    V3 oc = r.o - ld3(a);
+    float rad = b.x;
+    float A = dot(r.d, r.d);
+    float B = 2.0f * dot(oc, r.d);
+    float C = dot(oc, oc) - rad * rad;
+    float disc = (B * B - 4 * A * C);
+    const float y = 2 * A;
+#ifdef __HIP_DEVICE_COMPILE__
+    const float s0 = __builtin_amdgcn_sqrtf(disc);
+    const float sd = __uint_as_float(__float_as_uint(s0) - 1u), su = __uint_as_float(__float_as_uint(s0) + 1u);
+    const float rd = __builtin_fmaf(-sd, s0, disc), ru = __builtin_fmaf(-su, s0, disc);
+    float delta = ru > 0.0f ? su : (rd <= 0.0f ? sd : s0);
+    const float ry = rcp_rn(y);
+    float x1 = -B - delta, x2 = -B + delta;
+    float q1 = x1 * ry, q2 = x2 * ry;
+    float t1 = __builtin_fmaf(__builtin_fmaf(-y, q1, x1), ry, q1), t2 = __builtin_fmaf(__builtin_fmaf(-y, q2, x2), ry, q2);
+    const bool fast = disc >= 0x1p-96f && disc < 0x1p96f && in_range60(y) && in_range60(x1) && in_range60(x2);
+    if (__builtin_expect(disc > 0 && !fast, 0)) {
+        delta = sqrtf(B * B - 4 * A * C);
+        t1 = (-B - delta) / (2 * A);
+        t2 = (-B + delta) / (2 * A);
+    }
+#else
+    float delta = sqrtf(B * B - 4 * A * C);
+    float t1 = (-B - delta) / y, t2 = (-B + delta) / y;
+#endif
+    bool h1 = r.mint <= t1 && t1 <= r.maxt, h2 = r.mint <= t2 && t2 <= r.maxt;
+    t = h1 ? t1 : t2;
+    return (disc > 0) && (h1 || h2);
+}
+
 // Small scenes: wave-uniform scan of the primitive list.  Every lane tests
 // every primitive the wave needs in the same order, so the records arrive
 // through scalar loads and no lane diverges; the result is the closest hit.
@@ -395,7 +440,7 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float t = 0;
-            const bool h = sphere_hit_nb(p0, p1, r[k], t);  // t <= r.maxt = tb
+            const bool h = sphere_hit_fast(p0, p1, r[k], t);  // t <= r.maxt = tb
             if (h && live[k] && (ANY || t != tb[k] || pos > lb[k])) {
                 found[k] = true;
                 if (!ANY) {
@@ -671,6 +716,14 @@ ND SegRange seg_range_k(const uint32_t *cnt, uint32_t G, uint32_t K) {
     for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
     return r;
 }
+ND SegRange seg_range_per(const uint32_t *cnt, uint32_t G, uint32_t per) {  // `per` work-groups per group
+    SegRange r;
+    r.s0 = (blockIdx.x / per) * kTraceGroup;
+    r.pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
+    return r;
+}
 ND uint32_t seg_entry(const SegRange &r, uint32_t i) {
     uint32_t k = 0;
 #pragma unroll
@@ -775,14 +828,25 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
 #ifdef NORI_PROF_EXTEND
 static __device__ unsigned long long g_ext_prof[4];  // per wave: loads, scan, store clocks; waves
 #endif
+// Work-group sizes of the scan-mode extension and shadow kernels: 256
+// threads (C2 median 5176 against 5023 Msamples/s with 128; 512 makes the
+// extension launch slower, 0.0786 against 0.0752 ms).
+#ifndef NORI_EXTEND_BLOCK
+#define NORI_EXTEND_BLOCK 256
+#endif
+#ifndef NORI_SHADOW_BLOCK
+#define NORI_SHADOW_BLOCK 256
+#endif
+template <int K, uint32_t B>
+constexpr uint32_t scan_per() { return kTraceGroup * kSeg / (B * K); }  // work-groups per group
 template <int K>
-__global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
-                                                             uint32_t G) {
-    const SegRange sr = seg_range_k(cnt, G, K);
-    // a lane's K rays are entries kTraceBlock apart (adjacent entries, so
+__global__ __launch_bounds__(NORI_EXTEND_BLOCK) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
+                                                            uint32_t G) {
+    const SegRange sr = seg_range_per(cnt, G, scan_per<K, NORI_EXTEND_BLOCK>());
+    // a lane's K rays are entries NORI_EXTEND_BLOCK apart (adjacent entries, so
     // that a wave covers 64 K consecutive ones, measured 1 % slower)
-    constexpr uint32_t STEP = kTraceBlock;
-    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
+    constexpr uint32_t STEP = NORI_EXTEND_BLOCK;
+    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % scan_per<K, NORI_EXTEND_BLOCK>()) * NORI_EXTEND_BLOCK * K + threadIdx.x;
     if (i0 >= n) return;  // entries fill the slice from its start
     TRay r[K];
     bool live[K];
@@ -840,10 +904,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_extend_scan(DevScene S, PathQue
 }
 
 template <int K>
-__global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
-                                                             float4 *rec, uint32_t G) {
-    const SegRange sr = seg_range_k(shcnt, G, K);
-    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % (kTraceSlices / K)) * kTraceBlock * K + threadIdx.x;
+__global__ __launch_bounds__(NORI_SHADOW_BLOCK) void k_shadow_scan(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
+                                                            float4 *rec, uint32_t G) {
+    const SegRange sr = seg_range_per(shcnt, G, scan_per<K, NORI_SHADOW_BLOCK>());
+    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % scan_per<K, NORI_SHADOW_BLOCK>()) * NORI_SHADOW_BLOCK * K + threadIdx.x;
     if (i0 >= n) return;
     TRay r[K];
     bool live[K], valid[K];
@@ -853,7 +917,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_shadow_scan(DevScene S, ShadowQ
     float4 c[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint32_t i = i0 + k * kTraceBlock;
+        const uint32_t i = i0 + k * NORI_SHADOW_BLOCK;
         valid[k] = live[k] = i < n;
         q[k] = seg_entry(sr, live[k] ? i : i0);
         float4 a = sq.ray_o[q[k]], b = sq.ray_d[q[k]];
@@ -3011,7 +3075,7 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
                          hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
-        dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRays));
+        const dim3 gk((G + kTraceGroup - 1) / kTraceGroup * scan_per<kScanRays, NORI_EXTEND_BLOCK>()), bk(NORI_EXTEND_BLOCK);
         const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
         const int mode = extend_mode();
         const ShadowQueue nsq{nullptr, nullptr, nullptr};
@@ -3019,7 +3083,7 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
             hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
             return hipGetLastError();
         }
-        hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, b, 0, st, S, q, cnt, G);
+        hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
         if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK
             float4 *scratch = check_scratch((size_t)G * kSeg * sizeof(float4));
             if (!scratch) return hipErrorOutOfMemory;
@@ -3043,7 +3107,7 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
                          int stack, hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
     if (stack == 0) {
-        dim3 gk((G + kTraceGroup - 1) / kTraceGroup * (kTraceSlices / kScanRaysShadow));
+        const dim3 gk((G + kTraceGroup - 1) / kTraceGroup * scan_per<kScanRaysShadow, NORI_SHADOW_BLOCK>()), bk(NORI_SHADOW_BLOCK);
         const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
         const int mode = extend_mode();
         const PathQueue npq{nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -3057,7 +3121,7 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
             hipLaunchKernelGGL((k_trace_bin<true, true>), gb, bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
             hipLaunchKernelGGL(k_shadow_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, S, sq, shcnt, G, flags);
         }
-        hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, b, 0, st, S, sq, shcnt, rec, G);
+        hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, bk, 0, st, S, sq, shcnt, rec, G);
         return hipGetLastError();
     }
     switch (stack) {

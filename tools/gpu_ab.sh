@@ -1,10 +1,14 @@
 #!/bin/bash
 # Interleaved A/B benchmark: each configuration (an env assignment, "-" = none)
 # runs once per round for $REPS rounds; prints every value and the median.
-# usage: REPS=3 tools/gpu_ab.sh "- NORI_POOL_PARTS=1 NORI_POOL_PARTS=3,NORI_X=1" [bench args]
+# "@name" = NORI_GPU_LIB=<lib>/libnori_gpu_name.so (a variant build).
+# usage: REPS=3 tools/gpu_ab.sh "- NORI_POOL_PARTS=1 NORI_POOL_PARTS=3,NORI_X=1 @variant" [bench args]
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-cfgs=$1; shift
+L=$GRAFT_REPO_ROOT/nori-ray-tracer_amd/lib
+cfgs=""
+for c in $1; do case $c in @*) c="NORI_GPU_LIB=$L/libnori_gpu_${c#@}.so";; esac; cfgs="$cfgs $c"; done
+shift
 reps=${REPS:-3}
 for r in $(seq 1 $reps); do
   for c in $cfgs; do
