@@ -103,6 +103,10 @@ struct DevScene {
     float filter[NORI_FILTER_RESOLUTION + 1];
     float filter_radius, lookup;
     int32_t border;
+    // != 0 (= lookup, a power of two <= 64): a sample record's w word carries
+    // the sub-pixel class of its jitter (jit_class), from which k_splat reads
+    // the filter weights instead of re-deriving the jitter from pcg32
+    int32_t jit_lk;
     int32_t integrator;
     // 1: next-event estimation at a mirror/dielectric vertex only draws its
     // three random numbers (deviation D10; no environment-map emitter)

@@ -161,6 +161,39 @@ NHD V2 next2D(Pcg &r) {
     return s;
 }
 
+// ---------------------------------------------------------------- jitter classes
+// ImageBlock::put (block.cpp:93-122) places a sample of pixel x in block
+// offset ox at P = fl(fl(fl(x + jit) - 0.5) - (ox - border)) and weighs tile
+// cell c by filter[(int)(|c - P| * lookup)] when
+// ceil(P - r) <= c <= floor(P + r).  With a power-of-two radius r and lookup
+// factor every later step is exact -- c - P and f = P - floor(P) share P's grid
+// and are no larger, the products are by powers of two -- except
+// fl(P +- r), which can round across an integer only where |c - P| >= r,
+// i.e. at index NORI_FILTER_RESOLUTION, whose weight is 0.  So the weights of
+// the window cells depend only on (floor(P) - (x - ox) - border + 1 in {0, 1},
+// [f * lookup integer], q = floor(f * lookup)): for j = c - floor(P) >= 1
+// the index is j * lookup - ceil(f * lookup), for j <= 0 it is
+// |j| * lookup + q, and the box's ends are floor(P) + ceil(f - r) and
+// floor(P) + floor(f + r).  jit_class packs that triple into 8 bits
+// (lookup <= 64); k_splat expands a class into its weights with a
+// representative f of the same triple (tests/test_jit_class.py checks the
+// weights against the direct formula on every pixel column).
+constexpr uint32_t kRecPending = 0x80000000u;  // sample record w bit 31: the finisher splats it
+NHD uint32_t jit_class(uint32_t x, float jit, float lk, int border) {
+    const int ox = (int)(x / NORI_BLOCK_SIZE) * NORI_BLOCK_SIZE;
+    const float P = ((float)x + jit) - 0.5f - (float)(ox - border);
+    const float n = floorf(P), f = P - n, qf = f * lk, q = floorf(qf);
+    return (uint32_t)((int)n - ((int)x - ox) - border + 1) | (q == qf ? 2u : 0u) | (uint32_t)q << 2;
+}
+// The w word of a new sample record: both classes (S.jit_lk != 0) or 0.
+NHD float rec_code(int lk, int border, uint32_t x, uint32_t y, V2 jit) {
+    if (!lk) return 0.0f;
+    const uint32_t c = jit_class(x, jit.x, (float)lk, border) | jit_class(y, jit.y, (float)lk, border) << 8;
+    float w;
+    __builtin_memcpy(&w, &c, 4);
+    return w;
+}
+
 // ---------------------------------------------------------------- frames
 struct Frame {
     V3 s, t, n;

@@ -1921,7 +1921,7 @@ ND void regen_path(const DevScene &S, const WorkDesc &wd, uint32_t w, uint32_t p
     ps.beta = V3{1, 1, 1};
     ps.prev = -1.0f;
     ps.work = w;
-    rec[w] = make_float4(0, 0, 0, 0);
+    rec[w] = make_float4(0, 0, 0, rec_code(S.jit_lk, S.border, x, y, jit));
 }
 
 // Chromatic aberration: channel ps.chan's Li has ended, so the sample goes on
@@ -2163,7 +2163,7 @@ ND void splat_sample(const DevScene &S, float *film, Counters *C, uint32_t x, ui
 __global__ __launch_bounds__(kTraceBlock) void k_mark(PathQueue Q, SegState seg, int sel, float4 *rec) {
     const uint32_t sg = blockIdx.x >> 1, idx = (blockIdx.x & 1) * kTraceBlock + threadIdx.x;
     if (idx >= seg.cnt[sel][sg]) return;
-    rec[__float_as_uint(Q.ray_d[sg * kSeg + idx].w) & kWorkMask].w = 1.0f;
+    rec[__float_as_uint(Q.ray_d[sg * kSeg + idx].w) & kWorkMask].w = __uint_as_float(kRecPending);
 }
 
 #endif
@@ -2748,7 +2748,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_direct(DevScene S, WorkDesc wd,
             camera_sample(S, px, py, ap, -1, o, d, mn, mx);
             L = V3{1, 1, 1} * ob.template Li<INTEG>(rng, o, d, mn, mx);
         }
-        rec[w] = make_float4(L.x, L.y, L.z, 0.0f);
+        rec[w] = make_float4(L.x, L.y, L.z, rec_code(S.jit_lk, S.border, x, y, jit));
     }
     // ray counts: one atomic per wave
     uint32_t rc = ob.rc, rs = ob.rs;
@@ -2864,54 +2864,87 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 // the same (2B+1)^2 window around it, so the thread sums the filtered samples
 // of all its passes in registers and touches the LDS tile once per window
 // cell instead of once per sample and cell.
-template <int B>
-__global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 *rec, SplatDesc sd, float *film,
-                                                      Counters *C) {
-    constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1;
+// SPLIT: two lanes per pixel (adjacent lanes, the same record), the first
+// summing the R, G and the second the B, W windows -- half the registers per
+// lane (more waves per SIMD hide the record loads), each lane redoing only the
+// record's decode and weight reads (CODED).
+#ifndef NORI_SPLAT_SPLIT_BLOCK
+#define NORI_SPLAT_SPLIT_BLOCK 512
+#endif
+constexpr int kSplatSplitBlock = NORI_SPLAT_SPLIT_BLOCK;
+template <int B, bool CODED, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_splat(DevScene S, const float4 *rec,
+                                                                                  SplatDesc sd, float *film,
+                                                                                  Counters *C) {
+    constexpr int NT = SPLIT ? kSplatSplitBlock : kSplatBlock, NH = SPLIT ? 1 : 2;  // threads; pairs per lane
+    constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1, KP = (K + 3) / 4;  // float4s per weight row
     __shared__ float tile[TS * TS * 4];
     __shared__ float ftab[NORI_FILTER_RESOLUTION + 1];
+    __shared__ float4 wtab[CODED ? 256 * KP : 1];  // CODED: the window weights of every jitter class
     int4 bi = sd.blocks[blockIdx.x];
     const int ox = bi.x, oy = bi.y, bw = bi.z & 0xFFFF, bh = bi.z >> 16;
     const uint32_t off = (uint32_t)bi.w;
     const uint32_t p0 = blockIdx.y * sd.passes_per_wg, p1 = min(sd.passes, p0 + sd.passes_per_wg);
-    for (int i = threadIdx.x; i < TS * TS * 4; i += kSplatBlock) tile[i] = 0.0f;
+    for (int i = threadIdx.x; i < TS * TS * 4; i += NT) tile[i] = 0.0f;
     if (threadIdx.x <= NORI_FILTER_RESOLUTION) ftab[threadIdx.x] = S.filter[threadIdx.x];
     __syncthreads();
     const int npix = bw * bh;
     const float rad = S.filter_radius, lk = S.lookup;
+    if constexpr (CODED) {
+        // class (floor(P) - lx - B + 1, [f lk integer], q) -> the K weights of the window
+        // cells d = 0..K-1 (tile column lx + d), computed by the formula of
+        // the direct path below on a representative sub-pixel offset f of the
+        // class (q / lk or (q + 1/2) / lk: the same indices and box ends,
+        // device_math.h jit_class); P = lx + m + f with m = B + n - 1
+        float *wt = reinterpret_cast<float *>(wtab);
+        for (int i = threadIdx.x; i < 16 * S.jit_lk * KP; i += NT) {
+            const int c = i / (4 * KP), d = i - c * (4 * KP);
+            const int m = B + (c & 1) - 1, q = c >> 2;
+            const float f = (c & 2) ? (float)q / lk : ((float)q + 0.5f) / lk;
+            float wv = 0.0f;
+            if (d < K) {
+                const int lo = m + (int)ceilf(f - rad), hi = m + (int)floorf(f + rad);
+                const int k = min((int)(fabsf((float)(d - m) - f) * lk), NORI_FILTER_RESOLUTION);
+                wv = (d >= lo && d <= hi) ? ftab[k] : 0.0f;
+            }
+            wt[i] = wv;
+        }
+        __syncthreads();
+    }
     const uint64_t WH = (uint64_t)S.W * (uint64_t)S.H;
     uint32_t inval = 0;
-    for (int j = threadIdx.x; j < npix; j += kSplatBlock) {
+    for (int jj = threadIdx.x; jj < (SPLIT ? 2 : 1) * npix; jj += NT) {
+        const int j = SPLIT ? jj >> 1 : jj, h = SPLIT ? jj & 1 : 0;  // h: the lane's channel pair (SPLIT)
         const int ly = j / bw, lx = j - ly * bw, x = ox + lx, y = oy + ly;
-        // the window's RGBW sums as two packed pairs per cell (RG, BW): each
-        // half of a v_pk_mul_f32 / v_pk_add_f32 rounds as the scalar op does
+        // the window's RGBW sums as two packed pairs per cell (RG, BW; SPLIT:
+        // the lane's pair): each half of a v_pk_mul_f32 / v_pk_add_f32 rounds
+        // as the scalar op does
         typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 acc[K][K][2];
+        f2 acc[K][K][NH];
 #pragma unroll
         for (int a = 0; a < K; ++a)
 #pragma unroll
-            for (int c = 0; c < K; ++c) acc[a][c][0] = acc[a][c][1] = f2{0.0f, 0.0f};
+            for (int c = 0; c < K; ++c)
+#pragma unroll
+                for (int e = 0; e < NH; ++e) acc[a][c][e] = f2{0.0f, 0.0f};
         bool any = false;
         float vs[7] = {0, 0, 0, 0, 0, 0, 0};  // sample statistics of the pixel (sd.var)
         // the next NORI_SPLAT_DEPTH passes' records are in flight while this one is splatted
         float4 Lq[NORI_SPLAT_DEPTH];
 #pragma unroll
         for (int d = 0; d < NORI_SPLAT_DEPTH; ++d)
-            Lq[d] = p0 + d < p1 ? rec[(size_t)(p0 + d) * sd.M + off + j] : make_float4(0, 0, 0, 1);
+            Lq[d] = p0 + d < p1 ? rec[(size_t)(p0 + d) * sd.M + off + j] : make_float4(0, 0, 0, __uint_as_float(kRecPending));
         for (uint32_t p = p0; p < p1; ++p) {
             const float4 L = Lq[0];
 #pragma unroll
             for (int d = 0; d + 1 < NORI_SPLAT_DEPTH; ++d) Lq[d] = Lq[d + 1];
             if (p + NORI_SPLAT_DEPTH < p1) Lq[NORI_SPLAT_DEPTH - 1] = rec[(size_t)(p + NORI_SPLAT_DEPTH) * sd.M + off + j];
-            if (L.w != 0.0f) continue;  // pending: the finisher splats this sample
-            uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
-            Pcg r;
-            wave_seed(r, sd.seed, sid);
-            V2 jit = next2D(r);
+            const uint32_t code = __float_as_uint(L.w);
+            if (code & kRecPending) continue;  // the finisher splats this sample
             // Color3f::isValid (common.cpp:224-231): invalid samples are dropped
             bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
             if (!valid) {
-                ++inval;
+                inval += h == 0;
                 continue;
             }
             any = true;
@@ -2922,34 +2955,53 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
             vs[4] += L.y * L.y;
             vs[5] += L.z * L.z;
             vs[6] += 1.0f;
-            float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
-            int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
-            int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
             float wx[K], wy[K];
+            if constexpr (CODED) {
+                const float4 *tx = wtab + (code & 255u) * KP, *ty = wtab + ((code >> 8) & 255u) * KP;
 #pragma unroll
-            for (int d = 0; d < K; ++d) {
-                int cx = lx + d, cy = ly + d;  // tile column / row of window cell d
-                int kx = min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION);
-                int ky = min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION);
-                const float fx = ftab[kx], fy = ftab[ky];  // unconditional: no branch per cell
-                wx[d] = (cx >= x0 && cx <= x1) ? fx : 0.0f;
-                wy[d] = (cy >= y0 && cy <= y1) ? fy : 0.0f;
-            }
-            f2 lrg[K], lbw[K];  // Color4f(value) * wx (the row factor is shared by all rows)
+                for (int e = 0; e < KP; ++e) {
+                    const float4 a = tx[e], b = ty[e];
+                    const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-            for (int c = 0; c < K; ++c) {
-                lrg[c] = f2{L.x, L.y} * wx[c];
-                lbw[c] = f2{L.z, 1.0f} * wx[c];  // (1 * wx) = wx exactly
+                    for (int h = 0; h < 4; ++h)
+                        if (4 * e + h < K) {
+                            wx[4 * e + h] = av[h];
+                            wy[4 * e + h] = bv[h];
+                        }
+                }
+            } else {
+                uint64_t sid = (uint64_t)(sd.pass_begin + p) * WH + (uint64_t)y * S.W + x;
+                Pcg r;
+                wave_seed(r, sd.seed, sid);
+                V2 jit = next2D(r);
+                float px = ((float)x + jit.x) - 0.5f - (float)(ox - B), py = ((float)y + jit.y) - 0.5f - (float)(oy - B);
+                int x0 = max((int)ceilf(px - rad), 0), y0 = max((int)ceilf(py - rad), 0);
+                int x1 = min((int)floorf(px + rad), TS - 1), y1 = min((int)floorf(py + rad), TS - 1);
+#pragma unroll
+                for (int d = 0; d < K; ++d) {
+                    int cx = lx + d, cy = ly + d;  // tile column / row of window cell d
+                    int kx = min((int)(fabsf((float)cx - px) * lk), NORI_FILTER_RESOLUTION);
+                    int ky = min((int)(fabsf((float)cy - py) * lk), NORI_FILTER_RESOLUTION);
+                    const float fx = ftab[kx], fy = ftab[ky];  // unconditional: no branch per cell
+                    wx[d] = (cx >= x0 && cx <= x1) ? fx : 0.0f;
+                    wy[d] = (cy >= y0 && cy <= y1) ? fy : 0.0f;
+                }
             }
+            // Color4f(value) * wx (the row factor is shared by all rows); (1 * wx) = wx exactly
+            f2 lp[NH][K];
+            const f2 rg{L.x, L.y}, bw1{L.z, 1.0f};
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+#pragma unroll
+                for (int e = 0; e < NH; ++e) lp[e][c] = (SPLIT ? (h ? bw1 : rg) : (e ? bw1 : rg)) * wx[c];
 #pragma unroll
             for (int a = 0; a < K; ++a)
 #pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    acc[a][c][0] += lrg[c] * wy[a];
-                    acc[a][c][1] += lbw[c] * wy[a];
-                }
+                for (int c = 0; c < K; ++c)
+#pragma unroll
+                    for (int e = 0; e < NH; ++e) acc[a][c][e] += lp[e][c] * wy[a];
         }
-        if (any && sd.var) {
+        if (any && sd.var && h == 0) {
             float *v = sd.var + 8 * ((size_t)y * S.W + x);
             for (int k = 0; k < 7; ++k) atomicAdd(v + k, vs[k]);
         }
@@ -2958,13 +3010,15 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
             for (int a = 0; a < K; ++a)
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    float *t = tile + 4 * ((ly + a) * TS + (lx + c));
-                    const f2 rg = acc[a][c][0], bw = acc[a][c][1];
-                    if (bw.y != 0.0f || rg.x != 0.0f || rg.y != 0.0f || bw.x != 0.0f) {
-                        atomicAdd(t + 0, rg.x);
-                        atomicAdd(t + 1, rg.y);
-                        atomicAdd(t + 2, bw.x);
-                        atomicAdd(t + 3, bw.y);
+                    float *t = tile + 4 * ((ly + a) * TS + (lx + c)) + 2 * h;
+                    const f2 u = acc[a][c][0], v = acc[a][c][NH - 1];
+                    if (SPLIT ? (u.x != 0.0f || u.y != 0.0f) : (v.y != 0.0f || u.x != 0.0f || u.y != 0.0f || v.x != 0.0f)) {
+                        atomicAdd(t + 0, u.x);
+                        atomicAdd(t + 1, u.y);
+                        if (!SPLIT) {
+                            atomicAdd(t + 2, v.x);
+                            atomicAdd(t + 3, v.y);
+                        }
                     }
                 }
         }
@@ -2972,7 +3026,7 @@ __global__ __launch_bounds__(kSplatBlock) void k_splat(DevScene S, const float4 
     if (inval) atomicAdd(&C->invalid, (unsigned long long)inval);
     __syncthreads();
     const int rows = bh + 2 * B, cols = bw + 2 * B, FW = S.W + 2 * B;
-    for (int i = threadIdx.x; i < rows * cols; i += kSplatBlock) {
+    for (int i = threadIdx.x; i < rows * cols; i += NT) {
         int yy = i / cols, xx = i - yy * cols;
         const float *c = tile + 4 * (yy * TS + xx);
         float *f = film + 4 * ((size_t)(oy + yy) * FW + (ox + xx));
@@ -3274,18 +3328,38 @@ bool trav_stats_take(unsigned long long out[8]) {
 #endif
 }
 
+// NORI_SPLAT_SPLIT=0: one lane per pixel in the coded splat too.
+#ifndef NORI_SPLAT_SPLIT
+#define NORI_SPLAT_SPLIT 1
+#endif
+static bool splat_split() {
+    static const bool on = [] {
+        const char *e = std::getenv("NORI_SPLAT_SPLIT");
+        return e ? e[0] != '0' : NORI_SPLAT_SPLIT != 0;
+    }();
+    return on;
+}
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st) {
     if (nblocks == 0 || sd.passes == 0) return hipSuccess;
     dim3 g(nblocks, (sd.passes + sd.passes_per_wg - 1) / sd.passes_per_wg), b(kSplatBlock);
+    const bool coded = S.jit_lk != 0, split = coded && splat_split();
+    const dim3 b2(kSplatSplitBlock);
+#define NORI_SPLAT_CASE(b_)                                                                          \
+    case b_:                                                                                         \
+        if (split) hipLaunchKernelGGL((k_splat<b_, true, true>), g, b2, 0, st, S, rec, sd, film, C); \
+        else if (coded) hipLaunchKernelGGL((k_splat<b_, true>), g, b, 0, st, S, rec, sd, film, C);  \
+        else hipLaunchKernelGGL((k_splat<b_, false>), g, b, 0, st, S, rec, sd, film, C);            \
+        break;
     switch (S.border) {
-    case 0: hipLaunchKernelGGL(k_splat<0>, g, b, 0, st, S, rec, sd, film, C); break;
-    case 1: hipLaunchKernelGGL(k_splat<1>, g, b, 0, st, S, rec, sd, film, C); break;
-    case 2: hipLaunchKernelGGL(k_splat<2>, g, b, 0, st, S, rec, sd, film, C); break;
-    case 3: hipLaunchKernelGGL(k_splat<3>, g, b, 0, st, S, rec, sd, film, C); break;
-    case 4: hipLaunchKernelGGL(k_splat<4>, g, b, 0, st, S, rec, sd, film, C); break;
+    NORI_SPLAT_CASE(0)
+    NORI_SPLAT_CASE(1)
+    NORI_SPLAT_CASE(2)
+    NORI_SPLAT_CASE(3)
+    NORI_SPLAT_CASE(4)
     default: return hipErrorInvalidValue;
     }
+#undef NORI_SPLAT_CASE
     return hipGetLastError();
 }
 

@@ -96,6 +96,21 @@ static float filter_eval(const nori_camera_desc &c, float x) {
     return 0.0f;
 }
 static int film_border(const nori_camera_desc &c) { return (int)std::ceil(c.filter_radius - 0.5f); }
+// k_splat's weights from a jitter class (kernels.hip jit_class) need every
+// step of ImageBlock::put's index arithmetic exact: a power-of-two radius and
+// lookup factor (radius * lookup = NORI_FILTER_RESOLUTION), lookup <= 64 so
+// that a class fits 8 bits.  The reference's default radii (gaussian and
+// Mitchell 2, tent 1, box 0.5) qualify; other filters keep the pcg32 jitter.
+static bool pow2f(float v) {
+    int e = 0;
+    return v > 0.0f && std::frexp(v, &e) == 0.5f;
+}
+static int jit_code_lookup(float radius, float lookup) {
+    if (const char *e = std::getenv("NORI_JIT_CODE"); e && e[0] == '0') return 0;  // A/B
+    if (!pow2f(radius) || !pow2f(lookup) || lookup > 64.0f || radius * lookup != (float)NORI_FILTER_RESOLUTION)
+        return 0;
+    return (int)lookup;
+}
 static void filter_table(const nori_camera_desc &c, float *t) {
     for (int i = 0; i < NORI_FILTER_RESOLUTION; ++i) t[i] = filter_eval(c, (c.filter_radius * i) / NORI_FILTER_RESOLUTION);
     t[NORI_FILTER_RESOLUTION] = 0.0f;
@@ -920,6 +935,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.lookup = NORI_FILTER_RESOLUTION / cam.filter_radius;
     S.border = film_border(cam);
     if (S.border > 4) throw NoriException(NORI_ERR_UNSUPPORTED, "filter radius above 4.5 pixels");
+    S.jit_lk = jit_code_lookup(S.filter_radius, S.lookup);
     S.integrator = d.integrator;
     {  // deviation D10 (kernels.hip skip_nee); NORI_DISCRETE_NEE=1 keeps the full NEE everywhere
         bool env = false;
