@@ -171,7 +171,11 @@ def roofline(ts, samples, config="c2"):
                 row["valu_issue_frac"] = rate / VALU_PEAK
         rows[name] = row
     d = rows["k_extend"]
-    return {"bound": "hbm", "kernel": "k_extend", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS,
+    # the render's tail: the film splat (16 B record read per sample) beside the finisher
+    tail = {"ms_splat": ts.get("ms_splat", 0.0), "ms_finish": ts.get("ms_finish", 0.0)}
+    if tail["ms_splat"] > 0:
+        tail["splat_record_GBs"] = samples * 16 / (tail["ms_splat"] / 1e3) / 1e9
+    return {"tail": tail, "bound": "hbm", "kernel": "k_extend", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": d["frac"], "traffic": d.get("traffic_bytes_per_launch"), "traffic_profile": d.get("profile"),
             "bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": d["avg_launch_ms"], "launches": launches,
             "measured": "HIP events on the launch stream, one extra render after the timed region with one pool "

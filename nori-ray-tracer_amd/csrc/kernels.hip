@@ -87,6 +87,27 @@ ND void load_node(const DevScene &S, uint32_t ref, float4 &mnx, float4 &mny, flo
     rf = gld(nd + 6);
 }
 
+// 1 / det of the triangle tests: rcp_rn (NORI_SCAN_RCP_UNCHECKED, a
+// measurement build: without rcp_rn's range branch -- not exact for
+// |det| > 2^125).
+ND float rcp_det(float x) {
+#if defined(NORI_SCAN_RCP_UNCHECKED) && defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+#elif defined(NORI_RCP_WAVE) && defined(__HIP_DEVICE_COMPILE__)
+    // rcp_rn with its range test as one wave-uniform branch (no exec-mask
+    // save and restore around the common case)
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    float q = __builtin_fmaf(e, r, r);
+    const bool in = __builtin_fabsf(x) <= 0x1p125f;
+    if (__builtin_expect(!__all(in), 0)) q = in ? q : 1.0f / x;
+    return q;
+#else
+    return rcp_rn(x);
+#endif
+}
 // Mesh::rayIntersect (mesh.cpp:83-120), edges precomputed exactly.
 ND bool tri_hit(const float4 &a, const float4 &b, const float4 &c, const TRay &r, float &t, float &u, float &v) {
     V3 v0 = ld3(a), e1 = ld3(b), e2 = ld3(c);
@@ -128,7 +149,7 @@ ND bool tri_hit_nb(const float4 &a, const float4 &b, const float4 &c, const TRay
     V3 v0 = ld3(a), e1 = ld3(b), e2 = ld3(c);
     V3 pvec = cross(r.d, e2);
     float det = dot(e1, pvec);
-    float inv_det = rcp_rn(det);  // == 1.0f / det (tools/rcp_check.hip)
+    float inv_det = rcp_det(det);  // == 1.0f / det (tools/rcp_check.hip)
     V3 tvec = r.o - v0;
     u = dot(tvec, pvec) * inv_det;
     V3 qvec = cross(tvec, e1);
@@ -165,7 +186,7 @@ ND bool tri_hit_plane(const float4 &a, const float4 &b, const float4 &c, const T
         det = e1.x * pvec.x + e1.y * pvec.y;
         qvec = V3{-(tvec.z * e1.y), tvec.z * e1.x, tvec.x * e1.y - tvec.y * e1.x};
     }
-    const float inv_det = rcp_rn(det);
+    const float inv_det = rcp_det(det);
     u = dot(tvec, pvec) * inv_det;
     v = dot(d, qvec) * inv_det;
     t = (A == 0 ? e2.y * qvec.y + e2.z * qvec.z : A == 1 ? e2.x * qvec.x + e2.z * qvec.z : e2.x * qvec.x + e2.y * qvec.y) *
@@ -343,14 +364,39 @@ ND void scan_tri(const float4 &a, const float4 &b, const float4 &c, TRay (&r)[K]
 // (measured: the checks cost 7 % of the kernel's instructions and skip almost
 // nothing), while shadow rays, short segments towards the lights, skip most
 // walls.
+#ifdef NORI_CONST_SCENE
+// Measurement build (tools/gen_const_scene.py): one scene's scan list as
+// literal operands.  Renders only that scene correctly.
+#include "const_scene.h"
+ND float4 crec(uint32_t i) { return make_float4(kCRec[4 * i], kCRec[4 * i + 1], kCRec[4 * i + 2], kCRec[4 * i + 3]); }
+ND float4 cpf(uint32_t i) { return make_float4(kCPlaneF[4 * i], kCPlaneF[4 * i + 1], kCPlaneF[4 * i + 2], kCPlaneF[4 * i + 3]); }
+#define NORI_SC_PLANE_END(a) kCPlaneEnd[a]
+#define NORI_SC_PRIM(i) crec(i)
+#define NORI_SC_PLANE_F(i) cpf(i)
+#define NORI_SC_PLANE_C(g) kCPlaneC[g]
+#define NORI_SC_TRIS kCTris
+#define NORI_SC_REAL kCReal
+#define NORI_SC_PRIMS kCPrims
+#define NORI_SC_UNROLL _Pragma("unroll")
+#else
+#define NORI_SC_PLANE_END(a) S.plane_end[a]
+#define NORI_SC_PRIM(i) S.prims[i]
+#define NORI_SC_PLANE_F(i) S.plane_f[i]
+#define NORI_SC_PLANE_C(g) S.plane_c[g]
+#define NORI_SC_TRIS S.num_scan_tris
+#define NORI_SC_REAL S.num_scan_real
+#define NORI_SC_PRIMS S.num_prims
+#define NORI_SC_UNROLL
+#endif
 template <int A, int K, bool ANY, int CULL, bool GEN = false>
 ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                     uint32_t (&lb)[K], float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
-    const uint32_t g0 = A == 0 ? 0u : S.plane_end[A - 1], g1 = S.plane_end[A];
+    const uint32_t g0 = A == 0 ? 0u : NORI_SC_PLANE_END(A - 1), g1 = NORI_SC_PLANE_END(A);
+    NORI_SC_UNROLL
     for (uint32_t g = g0; g < g1; ++g) {
         if (CULL == 2) {  // the in-plane filter (pair_candidate): the whole rectangle, not only the plane
             constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
-            const float4 f0 = S.plane_f[2 * g], f1 = S.plane_f[2 * g + 1];
+            const float4 f0 = NORI_SC_PLANE_F(2 * g), f1 = NORI_SC_PLANE_F(2 * g + 1);
             bool may = false;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -362,7 +408,7 @@ ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], floa
             }
             if (!__any(may)) continue;
         } else if (CULL) {
-            const float c = S.plane_c[g];
+            const float c = NORI_SC_PLANE_C(g);
             bool may = false;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -372,10 +418,9 @@ ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], floa
             }
             if (!__any(may)) continue;
         }
-        const float4 *p = S.prims + 6 * (size_t)g;
         float4 q[6];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) q[j] = p[j];
+        for (int j = 0; j < 6; ++j) q[j] = NORI_SC_PRIM(6 * g + j);
         scan_tri<K, ANY, GEN ? -1 : A>(q[0], q[1], q[2], r, live, tb, pb, lb, ub, vb, found);
         scan_tri<K, ANY, GEN ? -1 : A>(q[3], q[4], q[5], r, live, tb, pb, lb, ub, vb, found);
     }
@@ -411,32 +456,32 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
         for (int k = 0; k < K; ++k) z = z || (live[k] && !(r[k].mint > 0.0f));
         gen = __any(z);
     }
-    if (S.plane_end[2] && !gen) {
+    if (NORI_SC_PLANE_END(2) && !gen) {
         scan_planes<0, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<1, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<2, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
-    } else if (ZMINT && S.plane_end[2]) {
+    } else if (ZMINT && NORI_SC_PLANE_END(2)) {
         scan_planes<0, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<1, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<2, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
     }
-    const uint32_t nt = S.num_scan_tris, n = S.num_prims, real = S.num_scan_real;
-    for (uint32_t i = 2 * S.plane_end[2]; i < nt; i += kScanGroup) {
+    const uint32_t nt = NORI_SC_TRIS, n = NORI_SC_PRIMS, real = NORI_SC_REAL;
+    NORI_SC_UNROLL
+    for (uint32_t i = 2 * NORI_SC_PLANE_END(2); i < nt; i += kScanGroup) {
         if (ANY && all_done()) return;
-        const float4 *p = S.prims + 3 * (size_t)i;
         float4 q[3 * kScanGroup];
 #pragma unroll
-        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) q[j] = p[j];
+        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) q[j] = NORI_SC_PRIM(3 * i + j);
 #pragma unroll
         for (uint32_t g = 0; g < kScanGroup; ++g)
             if (i + g < real)  // (the padding records never hit)
                 scan_tri<K, ANY>(q[3 * g], q[3 * g + 1], q[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
+    NORI_SC_UNROLL
     for (uint32_t i = nt; i < n; ++i) {
         if (ANY && all_done()) return;
-        const float4 *p = S.prims + 3 * (size_t)i;
-        const float4 p0 = p[0], p1 = p[1];
-        const uint32_t pos = __float_as_uint(p[2].w);
+        const float4 p0 = NORI_SC_PRIM(3 * i), p1 = NORI_SC_PRIM(3 * i + 1);
+        const uint32_t pos = __float_as_uint(NORI_SC_PRIM(3 * i + 2).w);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float t = 0;
@@ -839,9 +884,14 @@ static __device__ unsigned long long g_ext_prof[4];  // per wave: loads, scan, s
 #endif
 template <int K, uint32_t B>
 constexpr uint32_t scan_per() { return kTraceGroup * kSeg / (B * K); }  // work-groups per group
+#ifdef NORI_EXTEND_WAVES  // tuning: waves per SIMD the register allocation must allow
+#define NORI_EXTEND_ATTR __attribute__((amdgpu_waves_per_eu(NORI_EXTEND_WAVES)))
+#else
+#define NORI_EXTEND_ATTR
+#endif
 template <int K>
-__global__ __launch_bounds__(NORI_EXTEND_BLOCK) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
-                                                            uint32_t G) {
+__global__ __launch_bounds__(NORI_EXTEND_BLOCK) NORI_EXTEND_ATTR void k_extend_scan(DevScene S, PathQueue pq,
+                                                                                 const uint32_t *cnt, uint32_t G) {
     const SegRange sr = seg_range_per(cnt, G, scan_per<K, NORI_EXTEND_BLOCK>());
     // a lane's K rays are entries NORI_EXTEND_BLOCK apart (adjacent entries, so
     // that a wave covers 64 K consecutive ones, measured 1 % slower)
@@ -2871,12 +2921,16 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 #ifndef NORI_SPLAT_SPLIT_BLOCK
 #define NORI_SPLAT_SPLIT_BLOCK 512
 #endif
+#ifndef NORI_SPLAT_SPLIT_DEPTH
+#define NORI_SPLAT_SPLIT_DEPTH 8
+#endif
 constexpr int kSplatSplitBlock = NORI_SPLAT_SPLIT_BLOCK;
 template <int B, bool CODED, bool SPLIT = false>
 __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_splat(DevScene S, const float4 *rec,
                                                                                   SplatDesc sd, float *film,
                                                                                   Counters *C) {
     constexpr int NT = SPLIT ? kSplatSplitBlock : kSplatBlock, NH = SPLIT ? 1 : 2;  // threads; pairs per lane
+    constexpr int D = SPLIT ? NORI_SPLAT_SPLIT_DEPTH : NORI_SPLAT_DEPTH;           // records in flight per lane
     constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1, KP = (K + 3) / 4;  // float4s per weight row
     __shared__ float tile[TS * TS * 4];
     __shared__ float ftab[NORI_FILTER_RESOLUTION + 1];
@@ -2929,23 +2983,14 @@ __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_spla
                 for (int e = 0; e < NH; ++e) acc[a][c][e] = f2{0.0f, 0.0f};
         bool any = false;
         float vs[7] = {0, 0, 0, 0, 0, 0, 0};  // sample statistics of the pixel (sd.var)
-        // the next NORI_SPLAT_DEPTH passes' records are in flight while this one is splatted
-        float4 Lq[NORI_SPLAT_DEPTH];
-#pragma unroll
-        for (int d = 0; d < NORI_SPLAT_DEPTH; ++d)
-            Lq[d] = p0 + d < p1 ? rec[(size_t)(p0 + d) * sd.M + off + j] : make_float4(0, 0, 0, __uint_as_float(kRecPending));
-        for (uint32_t p = p0; p < p1; ++p) {
-            const float4 L = Lq[0];
-#pragma unroll
-            for (int d = 0; d + 1 < NORI_SPLAT_DEPTH; ++d) Lq[d] = Lq[d + 1];
-            if (p + NORI_SPLAT_DEPTH < p1) Lq[NORI_SPLAT_DEPTH - 1] = rec[(size_t)(p + NORI_SPLAT_DEPTH) * sd.M + off + j];
+        auto put = [&](const float4 &L, uint32_t p) {
             const uint32_t code = __float_as_uint(L.w);
-            if (code & kRecPending) continue;  // the finisher splats this sample
+            if (code & kRecPending) return;  // the finisher splats this sample
             // Color3f::isValid (common.cpp:224-231): invalid samples are dropped
             bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
             if (!valid) {
                 inval += h == 0;
-                continue;
+                return;
             }
             any = true;
             vs[0] += L.x;
@@ -3000,6 +3045,20 @@ __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_spla
                 for (int c = 0; c < K; ++c)
 #pragma unroll
                     for (int e = 0; e < NH; ++e) acc[a][c][e] += lp[e][c] * wy[a];
+        };
+        // the records of the next D passes are in flight while one is splatted
+        // (a ring of D registers, the pass loop unrolled by D: no moves)
+        float4 Lq[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            Lq[d] = p0 + d < p1 ? rec[(size_t)(p0 + d) * sd.M + off + j] : make_float4(0, 0, 0, __uint_as_float(kRecPending));
+        for (uint32_t p = p0; p < p1; p += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const float4 L = Lq[d];
+                if (p + D + d < p1) Lq[d] = rec[(size_t)(p + D + d) * sd.M + off + j];
+                if (p + d < p1) put(L, p + d);
+            }
         }
         if (any && sd.var && h == 0) {
             float *v = sd.var + 8 * ((size_t)y * S.W + x);

@@ -16,7 +16,7 @@ for r in $(seq 1 $reps); do
     env $envs timeout -k 10 300 python bench.py --no-cpu-baseline --no-parity "$@" > gpurun_out/ab.log 2>&1
     rc=$?; if [ $rc -ne 0 ]; then echo "$c rc=$rc"; tail -3 gpurun_out/ab.log; exit $rc; fi
     v=$(grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; print(round(json.loads(sys.stdin.read())['value'],1))")
-    grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()).get('roofline') or {}; print('   roofline frac', round(r.get('frac', 0), 4), {k: round(v['avg_launch_ms'], 4) for k, v in (r.get('kernels') or {}).items()})"
+    grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()).get('roofline') or {}; print('   roofline frac', round(r.get('frac', 0), 4), {k: round(v['avg_launch_ms'], 4) for k, v in (r.get('kernels') or {}).items()}, {k: round(v, 3) for k, v in (r.get('tail') or {}).items()})"
     echo "$c $v" | tee -a gpurun_out/ab_results.txt
     grep '^{' gpurun_out/ab.log | python3 -c "import json,sys; k=json.loads(sys.stdin.read()).get('kernel_ms',{}); print('   kernel_ms', {a: round(b,2) for a,b in k.items()})"
   done
