@@ -70,7 +70,9 @@ def main():
         path = os.path.join(d, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
-        for ctr in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
+        for ctr in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_INSTS_SMEM",
+                    "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_SCA",
+                    "SQ_INSTS_BRANCH", "SQ_BUSY_CYCLES", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
             for k, (n, v, ms) in per_kernel(path, ctr).items():
                 if k.startswith("__amd") or n == 0:
                     continue
