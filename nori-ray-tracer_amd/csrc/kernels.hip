@@ -1044,8 +1044,8 @@ __global__ __launch_bounds__(NORI_EXTEND_BLOCK) __attribute__((amdgpu_waves_per_
             if (NORI_CAMERA_CULL && Si.plane_f && __all(cam)) scan_rays<K, false, 2, false, true>(Si, r, live, t, p, u, v, f);
             else scan_rays<K, false, 0, false, true>(Si, r, live, t, p, u, v, f);
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (live[k]) pq.hit[cur.q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
+            for (int k = 0; k < K; ++k)  // (live[k] is false now also for rays that miss the scene box: stored too)
+                if (cur.i0 + k * STEP < cur.n) pq.hit[cur.q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
         }
         if (bn >= nb) break;
         b = bn;
@@ -1133,8 +1133,8 @@ __global__ __launch_bounds__(NORI_EXTEND_BLOCK) __attribute__((amdgpu_waves_per_
             if (NORI_CAMERA_CULL && Si.plane_f && __all(cam)) scan_rays<K, false, 2, false, true>(Si, r, live, t, p, u, v, f);
             else scan_rays<K, false, 0, false, true>(Si, r, live, t, p, u, v, f);
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (live[k]) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
+            for (int k = 0; k < K; ++k)  // (live[k] is false now also for rays that miss the scene box: stored too)
+                if (i0 + k * STEP < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
         }
         if (bn >= nb) break;
         b = bn;
@@ -3416,18 +3416,23 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
             hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
             return hipGetLastError();
         }
-        if (const uint32_t pg = extend_persist_grid(gk.x)) {
+        if (const uint32_t pg = mode == 2 ? 0u : extend_persist_grid(gk.x)) {
             if (extend_dma()) hipLaunchKernelGGL(k_extend_scan_l<kScanRays>, dim3(pg), bk, 0, st, S, q, cnt, G, gk.x);
             else hipLaunchKernelGGL(k_extend_scan_p<kScanRays>, dim3(pg), bk, 0, st, S, q, cnt, G, gk.x);
         } else {
             hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
         }
-        if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK
+        if (mode == 2 && (bin_ok(S) || extend_persist_grid(gk.x))) {  // NORI_EXTEND_CHECK
             float4 *scratch = check_scratch((size_t)G * kSeg * sizeof(float4));
             if (!scratch) return hipErrorOutOfMemory;
             PathQueue q2 = q;
             q2.hit = scratch;
-            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
+            if (const uint32_t pg = extend_persist_grid(gk.x)) {  // the persistent scan against k_extend_scan
+                if (extend_dma()) hipLaunchKernelGGL(k_extend_scan_l<kScanRays>, dim3(pg), bk, 0, st, S, q2, cnt, G, gk.x);
+                else hipLaunchKernelGGL(k_extend_scan_p<kScanRays>, dim3(pg), bk, 0, st, S, q2, cnt, G, gk.x);
+            } else {
+                hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
+            }
             hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
         }
         return hipGetLastError();
