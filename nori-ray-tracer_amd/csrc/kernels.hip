@@ -1003,11 +1003,13 @@ __global__ __launch_bounds__(NORI_EXTEND_BLOCK) __attribute__((amdgpu_waves_per_
             x.sr.pre[k + 1] = x.sr.pre[k] + (x.sr.s0 + k < G ? cnt[x.sr.s0 + k] : 0u);
         x.n = x.sr.pre[kTraceGroup];
         x.i0 = (bb % PER) * STEP * K + threadIdx.x;
-        // lanes past the end load the segment's first entry (allocated; unused)
+        // lanes past the end load the group's first slot (allocated, segment
+        // s0 < G; unused).  Not seg_entry(0): with every count of the group
+        // zero it maps entry 0 to segment s0 + 3, which may lie past G.
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t i = x.i0 + k * STEP;
-            x.q[k] = seg_entry(x.sr, i < x.n ? i : 0u);
+            x.q[k] = i < x.n ? seg_entry(x.sr, i) : x.sr.s0 * kSeg;
             x.o[k] = pq.ray_o[x.q[k]];
             x.d[k] = pq.ray_d[x.q[k]];
         }
@@ -1074,12 +1076,13 @@ __global__ __launch_bounds__(NORI_EXTEND_BLOCK) __attribute__((amdgpu_waves_per_
         n = sr.pre[kTraceGroup];
         i0 = (bb % PER) * STEP * K + threadIdx.x;
     };
-    // issue the DMA of a batch's rays (lanes past the end: the segment's first entry)
+    // issue the DMA of a batch's rays (lanes past the end: the group's first
+    // slot, as in k_extend_scan_p)
     auto dma = [&](const SegRange &sr, uint32_t n, uint32_t i0, uint32_t (&q)[K]) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t i = i0 + k * STEP;
-            q[k] = seg_entry(sr, i < n ? i : 0u);
+            q[k] = i < n ? seg_entry(sr, i) : sr.s0 * kSeg;
             __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(pq.ray_o + q[k]),
                                              (void __attribute__((address_space(3))) *)&s_ray[wv][2 * k][0], 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(pq.ray_d + q[k]),
