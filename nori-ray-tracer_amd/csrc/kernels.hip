@@ -380,31 +380,15 @@ ND float4 cpf(uint32_t i) { return make_float4(kCPlaneF[4 * i], kCPlaneF[4 * i +
 #define NORI_SC_UNROLL _Pragma("unroll")
 #else
 #define NORI_SC_PLANE_END(a) S.plane_end[a]
-#define NORI_SC_PRIM(i) sc_ld<CL>(S.prims + (i))
-#define NORI_SC_PLANE_F(i) sc_ld<CL>(S.plane_f + (i))
+#define NORI_SC_PRIM(i) S.prims[i]
+#define NORI_SC_PLANE_F(i) S.plane_f[i]
 #define NORI_SC_PLANE_C(g) S.plane_c[g]
 #define NORI_SC_TRIS S.num_scan_tris
 #define NORI_SC_REAL S.num_scan_real
 #define NORI_SC_PRIMS S.num_prims
 #define NORI_SC_UNROLL
 #endif
-// CL: the scene records are read through the constant address space, which
-// the compiler may load with scalar loads even after the kernel has stored
-// to global memory (the persistent scans store hits between two scans, and a
-// plain global load there cannot be proven unclobbered, so it becomes a
-// per-lane vector load).  Only for records in global memory (not an
-// LDS-staged scene).
-template <bool CL>
-ND float4 sc_ld(const float4 *p) {
-    if constexpr (CL) {
-        typedef float cf4 __attribute__((ext_vector_type(4)));
-        const cf4 v = *(const __attribute__((address_space(4))) cf4 *)p;
-        return make_float4(v.x, v.y, v.z, v.w);
-    } else {
-        return *p;
-    }
-}
-template <int A, int K, bool ANY, int CULL, bool GEN = false, bool CL = false>
+template <int A, int K, bool ANY, int CULL, bool GEN = false>
 ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                     uint32_t (&lb)[K], float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
     const uint32_t g0 = A == 0 ? 0u : NORI_SC_PLANE_END(A - 1), g1 = NORI_SC_PLANE_END(A);
@@ -446,7 +430,7 @@ ND void scan_planes(const DevScene &S, TRay (&r)[K], const bool (&live)[K], floa
 // a ray tests the pairs with the generic test -- tri_hit_plane returns the
 // same t except for the sign of an exactly zero t, which only mint <= 0 can
 // accept.
-template <int K, bool ANY, int CULL, bool ZMINT = false, bool CL = false>
+template <int K, bool ANY, int CULL, bool ZMINT = false>
 ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                   float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
     scan_prologue<K>(S, r, live);
@@ -476,13 +460,13 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
 #define NORI_SCAN_SKIP 0
 #endif
     if ((NORI_SCAN_SKIP & 1) == 0 && NORI_SC_PLANE_END(2) && !gen) {
-        scan_planes<0, K, ANY, CULL, false, CL>(S, r, live, tb, pb, lb, ub, vb, found);
-        scan_planes<1, K, ANY, CULL, false, CL>(S, r, live, tb, pb, lb, ub, vb, found);
-        scan_planes<2, K, ANY, CULL, false, CL>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<0, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<1, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<2, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
     } else if (ZMINT && NORI_SC_PLANE_END(2)) {
-        scan_planes<0, K, ANY, CULL, true, CL>(S, r, live, tb, pb, lb, ub, vb, found);
-        scan_planes<1, K, ANY, CULL, true, CL>(S, r, live, tb, pb, lb, ub, vb, found);
-        scan_planes<2, K, ANY, CULL, true, CL>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<0, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<1, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
+        scan_planes<2, K, ANY, CULL, true>(S, r, live, tb, pb, lb, ub, vb, found);
     }
     const uint32_t nt = NORI_SC_TRIS, n = NORI_SC_PRIMS, real = NORI_SC_REAL;
     NORI_SC_UNROLL
@@ -523,10 +507,10 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
 // gives the VALU K independent dependency chains to interleave.  Results are
 // those of traverse<0, ANY> ray by ray.  CULL: the wave-wide plane skips
 // (every caller but the extension kernel, whose waves are incoherent).
-template <int K, bool ANY, int CULL = 1, bool ZMINT = false, bool CL = false>
+template <int K, bool ANY, int CULL = 1, bool ZMINT = false>
 ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[K], uint32_t (&pb)[K],
                   float (&ub)[K], float (&vb)[K], bool (&found)[K]) {
-    scan_core<K, ANY, CULL, ZMINT, CL>(S, r, live, tb, pb, ub, vb, found);
+    scan_core<K, ANY, CULL, ZMINT>(S, r, live, tb, pb, ub, vb, found);
 }
 
 // Primitive records fetched per memory round trip in a BVH leaf.
@@ -970,183 +954,6 @@ __global__ __launch_bounds__(NORI_EXTEND_BLOCK) NORI_EXTEND_ATTR void k_extend_s
         atomicAdd(&g_ext_prof[3], 1ull);
     }
 #endif
-}
-
-// Persistent form of k_extend_scan (NORI_EXTEND_PERSIST): a grid of about
-// the resident work-groups strides over the launch's batches (batch b = the
-// work-group k_extend_scan would have run as blockIdx b), and every wave
-// issues the next batch's ray loads before it scans the current one.  A
-// launch of short waves alternates between loading rays (memory busy, VALU
-// idle) and scanning them (the reverse): waves start in step, so their load
-// phases coincide (measured: the launch spends about as long as it would
-// take to move its 48 B per ray at 6 TB/s on top of its scan).  Here a wave's
-// loads overlap its own previous scan.  Same entries, same per-ray code:
-// the hit records are those of k_extend_scan.
-#ifndef NORI_EXTEND_PWAVES  // waves per SIMD the persistent scan's registers must allow
-#define NORI_EXTEND_PWAVES 6
-#endif
-template <int K>
-__global__ __launch_bounds__(NORI_EXTEND_BLOCK) __attribute__((amdgpu_waves_per_eu(NORI_EXTEND_PWAVES))) void k_extend_scan_p(DevScene S, PathQueue pq,
-                                                                                   const uint32_t *cnt, uint32_t G,
-                                                                                   uint32_t nb) {
-    constexpr uint32_t PER = scan_per<K, NORI_EXTEND_BLOCK>(), STEP = NORI_EXTEND_BLOCK;
-    struct Batch {
-        SegRange sr;
-        uint32_t n, i0, q[K];
-        float4 o[K], d[K];
-    };
-    auto fetch = [&](uint32_t bb, Batch &x) {
-        x.sr.s0 = (bb / PER) * kTraceGroup;
-        x.sr.pre[0] = 0;
-#pragma unroll
-        for (int k = 0; k < kTraceGroup; ++k)
-            x.sr.pre[k + 1] = x.sr.pre[k] + (x.sr.s0 + k < G ? cnt[x.sr.s0 + k] : 0u);
-        x.n = x.sr.pre[kTraceGroup];
-        x.i0 = (bb % PER) * STEP * K + threadIdx.x;
-        // lanes past the end load the group's first slot (allocated, segment
-        // s0 < G; unused).  Not seg_entry(0): with every count of the group
-        // zero it maps entry 0 to segment s0 + 3, which may lie past G.
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t i = x.i0 + k * STEP;
-            x.q[k] = i < x.n ? seg_entry(x.sr, i) : x.sr.s0 * kSeg;
-            x.o[k] = pq.ray_o[x.q[k]];
-            x.d[k] = pq.ray_d[x.q[k]];
-        }
-    };
-    uint32_t b = blockIdx.x;
-    if (b >= nb) return;
-    Batch cur;
-    fetch(b, cur);
-    for (;;) {
-        const uint32_t bn = b + gridDim.x;
-        Batch nxt;
-        if (bn < nb) fetch(bn, nxt);  // in flight during this batch's scan
-        if (__any(cur.i0 < cur.n)) {
-            TRay r[K];
-            bool live[K];
-            bool cam = true;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                live[k] = cur.i0 + k * STEP < cur.n;
-                path_ray(S, cur.o[k], cur.d[k], r[k]);
-                cam = cam && (!live[k] || (__float_as_uint(cur.d[k].w) & kCameraRay) != 0u);
-            }
-            float t[K], u[K], v[K];
-            uint32_t p[K];
-            bool f[K];
-            // the records through the constant address space (scalar loads,
-            // sc_ld), kept inside the loop: hoisted out of it -- they are
-            // loop-invariant -- they would pin more scalar registers than
-            // there are and spill into vector ones
-            DevScene Si = S;
-            const uint32_t z = b >> 31;  // 0, not provably so
-            Si.prims += z;
-            Si.plane_f += z;
-            if (NORI_CAMERA_CULL && Si.plane_f && __all(cam)) scan_rays<K, false, 2, false, true>(Si, r, live, t, p, u, v, f);
-            else scan_rays<K, false, 0, false, true>(Si, r, live, t, p, u, v, f);
-#pragma unroll
-            for (int k = 0; k < K; ++k)  // (live[k] is false now also for rays that miss the scene box: stored too)
-                if (cur.i0 + k * STEP < cur.n) pq.hit[cur.q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
-        }
-        if (bn >= nb) break;
-        b = bn;
-        cur = nxt;
-    }
-}
-
-// k_extend_scan_p with the next batch's rays prefetched into LDS by the
-// gfx950 LDS-DMA load (global_load_lds_dwordx4: 16 B per lane straight into
-// the wave's 4-KB LDS region, no registers held across the scan): a batch's
-// rays are read from LDS into registers, the DMA of the next batch is issued
-// into the same region, then the batch is scanned (NORI_EXTEND_PERSIST with
-// NORI_EXTEND_DMA=1).
-template <int K>
-__global__ __launch_bounds__(NORI_EXTEND_BLOCK) __attribute__((amdgpu_waves_per_eu(NORI_EXTEND_PWAVES))) void k_extend_scan_l(DevScene S, PathQueue pq,
-                                                                                   const uint32_t *cnt, uint32_t G,
-                                                                                   uint32_t nb) {
-    constexpr uint32_t PER = scan_per<K, NORI_EXTEND_BLOCK>(), STEP = NORI_EXTEND_BLOCK, NW = NORI_EXTEND_BLOCK / 64;
-    __shared__ float4 s_ray[NW][2 * K][64];  // per wave: (o, d) of ray 0, (o, d) of ray 1, ...
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    auto geom = [&](uint32_t bb, SegRange &sr, uint32_t &n, uint32_t &i0) {
-        sr.s0 = (bb / PER) * kTraceGroup;
-        sr.pre[0] = 0;
-#pragma unroll
-        for (int k = 0; k < kTraceGroup; ++k) sr.pre[k + 1] = sr.pre[k] + (sr.s0 + k < G ? cnt[sr.s0 + k] : 0u);
-        n = sr.pre[kTraceGroup];
-        i0 = (bb % PER) * STEP * K + threadIdx.x;
-    };
-    // issue the DMA of a batch's rays (lanes past the end: the group's first
-    // slot, as in k_extend_scan_p)
-    auto dma = [&](const SegRange &sr, uint32_t n, uint32_t i0, uint32_t (&q)[K]) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t i = i0 + k * STEP;
-            q[k] = i < n ? seg_entry(sr, i) : sr.s0 * kSeg;
-            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(pq.ray_o + q[k]),
-                                             (void __attribute__((address_space(3))) *)&s_ray[wv][2 * k][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(pq.ray_d + q[k]),
-                                             (void __attribute__((address_space(3))) *)&s_ray[wv][2 * k + 1][0], 16, 0, 0);
-        }
-    };
-    uint32_t b = blockIdx.x;
-    if (b >= nb) return;
-    SegRange sr;
-    uint32_t n, i0, q[K];
-    geom(b, sr, n, i0);
-    dma(sr, n, i0, q);
-    for (;;) {
-        __builtin_amdgcn_s_waitcnt(0);  // this batch's rays are in LDS (and every earlier store is done)
-        float4 o[K], d[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            o[k] = s_ray[wv][2 * k][lane];
-            d[k] = s_ray[wv][2 * k + 1][lane];
-        }
-        const uint32_t bn = b + gridDim.x;
-        SegRange srn;
-        uint32_t nn = 0, i0n = 0, qn[K];
-        if (bn < nb) {
-            geom(bn, srn, nn, i0n);
-            // the reads above must have returned before the DMA overwrites the region
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-            dma(srn, nn, i0n, qn);
-        }
-        if (__any(i0 < n)) {
-            TRay r[K];
-            bool live[K];
-            bool cam = true;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                live[k] = i0 + k * STEP < n;
-                path_ray(S, o[k], d[k], r[k]);
-                cam = cam && (!live[k] || (__float_as_uint(d[k].w) & kCameraRay) != 0u);
-            }
-            float t[K], u[K], v[K];
-            uint32_t p[K];
-            bool f[K];
-            // the records through the constant address space (scalar loads,
-            // sc_ld), kept inside the loop: hoisted out of it -- they are
-            // loop-invariant -- they would pin more scalar registers than
-            // there are and spill into vector ones
-            DevScene Si = S;
-            const uint32_t z = b >> 31;  // 0, not provably so
-            Si.prims += z;
-            Si.plane_f += z;
-            if (NORI_CAMERA_CULL && Si.plane_f && __all(cam)) scan_rays<K, false, 2, false, true>(Si, r, live, t, p, u, v, f);
-            else scan_rays<K, false, 0, false, true>(Si, r, live, t, p, u, v, f);
-#pragma unroll
-            for (int k = 0; k < K; ++k)  // (live[k] is false now also for rays that miss the scene box: stored too)
-                if (i0 + k * STEP < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
-        }
-        if (bn >= nb) break;
-        b = bn;
-        sr = srn;
-        n = nn;
-        i0 = i0n;
-#pragma unroll
-        for (int k = 0; k < K; ++k) q[k] = qn[k];
-    }
 }
 
 template <int K>
@@ -3380,33 +3187,6 @@ static float4 *check_scratch(size_t bytes) {
     }
     return p;
 }
-// NORI_EXTEND_PERSIST=w (w work-groups per CU; 0 = off): the persistent
-// extension scan k_extend_scan_p over min(batches, CUs * w) work-groups.
-#ifndef NORI_EXTEND_PERSIST
-#define NORI_EXTEND_PERSIST 0
-#endif
-static uint32_t extend_persist_grid(uint32_t batches) {
-    static const uint32_t wgs = [] {
-        const char *e = std::getenv("NORI_EXTEND_PERSIST");
-        const long w = e ? std::atol(e) : (long)NORI_EXTEND_PERSIST;
-        if (w <= 0) return 0u;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return (uint32_t)(w * cus);
-    }();
-    return wgs ? std::min(wgs, batches) : 0u;
-}
-#ifndef NORI_EXTEND_DMA
-#define NORI_EXTEND_DMA 1
-#endif
-static bool extend_dma() {
-    static const bool on = [] {
-        const char *e = std::getenv("NORI_EXTEND_DMA");
-        return e ? e[0] != '0' : NORI_EXTEND_DMA != 0;
-    }();
-    return on;
-}
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
     dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
@@ -3419,23 +3199,13 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
             hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
             return hipGetLastError();
         }
-        if (const uint32_t pg = mode == 2 ? 0u : extend_persist_grid(gk.x)) {
-            if (extend_dma()) hipLaunchKernelGGL(k_extend_scan_l<kScanRays>, dim3(pg), bk, 0, st, S, q, cnt, G, gk.x);
-            else hipLaunchKernelGGL(k_extend_scan_p<kScanRays>, dim3(pg), bk, 0, st, S, q, cnt, G, gk.x);
-        } else {
-            hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
-        }
-        if (mode == 2 && (bin_ok(S) || extend_persist_grid(gk.x))) {  // NORI_EXTEND_CHECK
+        hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
+        if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK
             float4 *scratch = check_scratch((size_t)G * kSeg * sizeof(float4));
             if (!scratch) return hipErrorOutOfMemory;
             PathQueue q2 = q;
             q2.hit = scratch;
-            if (const uint32_t pg = extend_persist_grid(gk.x)) {  // the persistent scan against k_extend_scan
-                if (extend_dma()) hipLaunchKernelGGL(k_extend_scan_l<kScanRays>, dim3(pg), bk, 0, st, S, q2, cnt, G, gk.x);
-                else hipLaunchKernelGGL(k_extend_scan_p<kScanRays>, dim3(pg), bk, 0, st, S, q2, cnt, G, gk.x);
-            } else {
-                hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
-            }
+            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
             hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
         }
         return hipGetLastError();
