@@ -53,7 +53,7 @@ from nori_amd._abi import BLOCK_SIZE  # noqa: E402
 
 METRIC = "Msamples/sec on cbox_path_mis 512×512@512spp; per-pixel L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PROFILE_TAG = "r04"  # committed rocprofv3 evidence: profiles/pmc_<tag>[_<config>].json (tools/pmc_to_profile.py)
+PROFILE_TAG = "r05"  # committed rocprofv3 evidence: profiles/pmc_<tag>[_<config>].json (tools/pmc_to_profile.py)
 VALU_PEAK = 256 * 4 * 2.4e9 / 2 * 64  # lane-instr/s: 256 CUs x 4 SIMDs, a wave64 VALU op per 2 cycles
 
 
