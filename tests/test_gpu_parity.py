@@ -161,6 +161,34 @@ def test_render_pass_split_and_pool_invariance(cbox):
     assert np.allclose(whole, part, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("filt", ["gaussian", "mitchell", "tent", "box"])  # radii 2, 2, 1, 1/2
+def test_splat_jitter_classes_match_the_pcg_jitter(built, tmp_path, filt):
+    """k_splat reading the filter weights from the records' jitter classes
+    (device_math.h jit_class) against re-deriving the jitter from pcg32
+    (NORI_JIT_CODE=0): the same weights, so the same film up to the order of
+    the tile atomics."""
+    src = open(scene_path("pa4", "cbox", "cbox_path_mis.xml")).read()
+    rf = f'<rfilter type="{filt}"/>'
+    xml = tmp_path / "cbox_filter.xml"
+    xml.write_text(src.replace("<camera type=\"perspective\">", "<camera type=\"perspective\">" + rf, 1))
+    s = nori_amd.load_scene(str(xml), 72, 56, 8)
+    films = []
+    for code in ("1", "0"):
+        old = os.environ.get("NORI_JIT_CODE")
+        os.environ["NORI_JIT_CODE"] = code
+        try:
+            with nori_amd.GpuRenderer(s, 0) as r:
+                films.append(r.render())
+        finally:
+            if old is None:
+                os.environ.pop("NORI_JIT_CODE")
+            else:
+                os.environ["NORI_JIT_CODE"] = old
+    a, b = films
+    assert a.shape == b.shape and np.isfinite(a).all()
+    assert np.abs(a - b).max() <= 1e-6 * np.abs(b).max(), np.abs(a - b).max()
+
+
 def test_render_block_subsets_tile_the_frame(cbox):
     s, r, o = cbox
     whole = r.render(passes=4)
