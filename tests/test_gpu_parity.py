@@ -167,7 +167,8 @@ def test_splat_jitter_classes_match_the_pcg_jitter(built, tmp_path, filt):
     (device_math.h jit_class) against re-deriving the jitter from pcg32
     (NORI_JIT_CODE=0): the same weights, so the same film up to the order of
     the tile atomics."""
-    src = open(scene_path("pa4", "cbox", "cbox_path_mis.xml")).read()
+    path = scene_path("pa4", "cbox", "cbox_path_mis.xml")
+    src = open(path).read().replace('name="filename" value="', f'name="filename" value="{os.path.dirname(path)}/')
     rf = f'<rfilter type="{filt}"/>'
     xml = tmp_path / "cbox_filter.xml"
     xml.write_text(src.replace("<camera type=\"perspective\">", "<camera type=\"perspective\">" + rf, 1))
