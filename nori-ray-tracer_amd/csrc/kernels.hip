@@ -2927,6 +2927,9 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 #ifndef NORI_SPLAT_SPLIT_DEPTH
 #define NORI_SPLAT_SPLIT_DEPTH 8
 #endif
+#ifndef NORI_SPLAT_NB
+#define NORI_SPLAT_NB 0
+#endif
 constexpr int kSplatSplitBlock = NORI_SPLAT_SPLIT_BLOCK;
 template <int B, bool CODED, bool SPLIT = false>
 __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_splat(DevScene S, const float4 *rec,
@@ -2934,6 +2937,7 @@ __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_spla
                                                                                   Counters *C) {
     constexpr int NT = SPLIT ? kSplatSplitBlock : kSplatBlock, NH = SPLIT ? 1 : 2;  // threads; pairs per lane
     constexpr int D = SPLIT ? NORI_SPLAT_SPLIT_DEPTH : NORI_SPLAT_DEPTH;           // records in flight per lane
+    constexpr bool NB = CODED && NORI_SPLAT_NB;  // per-sample checks as selects, not branches
     constexpr int TS = NORI_BLOCK_SIZE + 2 * B, K = 2 * B + 1, KP = (K + 3) / 4;  // float4s per weight row
     __shared__ float tile[TS * TS * 4];
     __shared__ float ftab[NORI_FILTER_RESOLUTION + 1];
@@ -2986,23 +2990,32 @@ __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_spla
                 for (int e = 0; e < NH; ++e) acc[a][c][e] = f2{0.0f, 0.0f};
         bool any = false;
         float vs[7] = {0, 0, 0, 0, 0, 0, 0};  // sample statistics of the pixel (sd.var)
-        auto put = [&](const float4 &L, uint32_t p) {
-            const uint32_t code = __float_as_uint(L.w);
-            if (code & kRecPending) return;  // the finisher splats this sample
-            // Color3f::isValid (common.cpp:224-231): invalid samples are dropped
-            bool valid = !(L.x < 0 || !isfinite(L.x) || L.y < 0 || !isfinite(L.y) || L.z < 0 || !isfinite(L.z));
-            if (!valid) {
-                inval += h == 0;
-                return;
+        auto put = [&](const float4 &L0, uint32_t p) {
+            const uint32_t code = __float_as_uint(L0.w);
+            // pending: the finisher splats this sample; Color3f::isValid
+            // (common.cpp:224-231): invalid samples are dropped
+            const bool pend = (code & kRecPending) != 0u;
+            const bool valid = !(L0.x < 0 || !isfinite(L0.x) || L0.y < 0 || !isfinite(L0.y) || L0.z < 0 || !isfinite(L0.z));
+            const bool ok = !pend && valid;
+            if constexpr (!NB) {
+                if (!ok) {
+                    inval += (!pend && h == 0) ? 1u : 0u;
+                    return;
+                }
+            } else {
+                inval += (!pend && !valid && h == 0) ? 1u : 0u;
             }
-            any = true;
+            // NB: a skipped sample adds exact zeros -- radiance 0 and weights
+            // 0 -- so the window sums keep their values bit for bit
+            const float4 L = make_float4(ok ? L0.x : 0.0f, ok ? L0.y : 0.0f, ok ? L0.z : 0.0f, 0.0f);
+            any = any || ok;
             vs[0] += L.x;
             vs[1] += L.y;
             vs[2] += L.z;
             vs[3] += L.x * L.x;
             vs[4] += L.y * L.y;
             vs[5] += L.z * L.z;
-            vs[6] += 1.0f;
+            vs[6] += ok ? 1.0f : 0.0f;
             float wx[K], wy[K];
             if constexpr (CODED) {
                 const float4 *tx = wtab + (code & 255u) * KP, *ty = wtab + ((code >> 8) & 255u) * KP;
@@ -3011,10 +3024,10 @@ __global__ __launch_bounds__(SPLIT ? kSplatSplitBlock : kSplatBlock) void k_spla
                     const float4 a = tx[e], b = ty[e];
                     const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-                    for (int h = 0; h < 4; ++h)
-                        if (4 * e + h < K) {
-                            wx[4 * e + h] = av[h];
-                            wy[4 * e + h] = bv[h];
+                    for (int c4 = 0; c4 < 4; ++c4)
+                        if (4 * e + c4 < K) {
+                            wx[4 * e + c4] = av[c4];
+                            wy[4 * e + c4] = ok ? bv[c4] : 0.0f;
                         }
                 }
             } else {
