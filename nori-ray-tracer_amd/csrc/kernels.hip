@@ -2917,6 +2917,10 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 // the same (2B+1)^2 window around it, so the thread sums the filtered samples
 // of all its passes in registers and touches the LDS tile once per window
 // cell instead of once per sample and cell.
+// CODED (S.jit_lk != 0): the sample's window weights come from the jitter
+// class its record carries (device_math.h jit_class), one row of a class
+// table built per work-group -- the same weights as re-deriving the jitter
+// from the sample's pcg32 stream (CODED = false), without the stream.
 // SPLIT: two lanes per pixel (adjacent lanes, the same record), the first
 // summing the R, G and the second the B, W windows -- half the registers per
 // lane (more waves per SIMD hide the record loads), each lane redoing only the
