@@ -2925,17 +2925,17 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 // summing the R, G and the second the B, W windows -- half the registers per
 // lane (more waves per SIMD hide the record loads), each lane redoing only the
 // record's decode and weight reads (CODED).
-// 768 threads (3 waves per SIMD) with 2 records in flight per lane: 100
+// 768 threads (3 waves per SIMD) with 4 records in flight per lane: 108
 // VGPRs, so that a 144-VGPR finisher wave still fits beside three splat
-// waves on a SIMD (3 x 104 + 144 <= 512).  Measured (C2): splat 1.17-1.20 ms
-// and finisher 1.15 ms against 1.26-1.33 / 1.10-1.15 ms for 512 threads with
-// 8 records; 768 threads with 8 records (136 VGPRs) splat in 0.83 ms but
-// starve the finisher (1.75 ms), DESIGN.md section 5.
+// waves on a SIMD (3 x 112 + 144 <= 512).  Measured (C2): splat 1.14-1.18 ms
+// and finisher 1.15-1.17 ms against 1.26-1.33 / 1.10-1.15 ms for 512 threads
+// with 8 records; 768 threads with 8 records (136 VGPRs) splat in 0.83 ms
+// but starve the finisher (1.75 ms), DESIGN.md section 5.
 #ifndef NORI_SPLAT_SPLIT_BLOCK
 #define NORI_SPLAT_SPLIT_BLOCK 768
 #endif
 #ifndef NORI_SPLAT_SPLIT_DEPTH
-#define NORI_SPLAT_SPLIT_DEPTH 2
+#define NORI_SPLAT_SPLIT_DEPTH 4
 #endif
 #ifndef NORI_SPLAT_NB
 #define NORI_SPLAT_NB 0
