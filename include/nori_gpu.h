@@ -51,7 +51,10 @@
 extern "C" {
 #endif
 
-#define NORI_GPU_ABI_VERSION 5
+/* Bumped whenever an exported signature or a shared struct changes (6: the
+ * leading status argument of nori_gpu_comm_timeout); the Python binding and
+ * the C++ adapter refuse a library of another version. */
+#define NORI_GPU_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 #define NORI_OK               0

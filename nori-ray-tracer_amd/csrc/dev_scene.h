@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "device_math.h"
+#include "seg_index.h"
 
 namespace nori {
 
@@ -82,6 +83,12 @@ struct DevScene {
     // per pair: the in-plane filter of k_extend_bin (runtime.hip plane_filters)
     const float4 *plane_f;
     uint32_t plane_end[3];
+    // run-time switches of the scan's exact wall-pair skips (nori_gpu_create:
+    // NORI_CAMERA_CULL, NORI_TRACE_CULL): camera_cull != 0 -- k_extend_scan
+    // filters the pairs of a wave of camera rays by the in-plane test
+    // (pair_candidate); trace_cull -- the trace API's scan: 0 tests every
+    // pair, 1 the plane-distance skip (plane_may_hit), 2 the in-plane filter
+    int32_t camera_cull, trace_cull;
     float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;
     float invW, invH;
@@ -178,7 +185,6 @@ struct ShadowQueue {
 // global atomics are needed to compact.  Work ids reach a segment through a
 // static stream of 256-id chunks (consecutive ids = adjacent pixels of one
 // 32x32 block, so a segment traces coherent camera rays).
-constexpr uint32_t kSeg = 256;
 #ifndef NORI_SCAN_GROUP
 #define NORI_SCAN_GROUP 4
 #endif

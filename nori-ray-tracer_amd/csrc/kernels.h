@@ -15,10 +15,6 @@ constexpr int kTraceSpill = 64;    // traversal stack entries beyond the LDS par
 // Stack entries held in LDS for an LDS budget of `stack` words per lane: with
 // NORI_STACK_KEYS each entry is a (child ref, entry distance) pair.
 constexpr int stack_lds_entries(int stack) { return NORI_STACK_KEYS ? stack / 2 : stack; }
-#ifndef NORI_TRACE_GROUP
-#define NORI_TRACE_GROUP 4
-#endif
-constexpr int kTraceGroup = NORI_TRACE_GROUP;  // segments per extend/shadow work-group
 constexpr int kSplatBlock = 256;
 #ifndef NORI_SCAN_RAYS
 #define NORI_SCAN_RAYS 2
@@ -53,7 +49,8 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
                          hipStream_t st);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st);
-// Marks the record of every queued path pending (w = 1): k_splat skips it.
+// Marks the record of every queued path pending (w = kRecPending, the jitter
+// class bits cleared): k_splat skips it, the finisher splats it itself.
 // Zeroes the counters and segment state of a chunk, Counters::exhausted = empty.
 hipError_t launch_reset(Counters *C, uint32_t empty, const SegState &seg, uint32_t G, hipStream_t st);
 hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st);
@@ -80,11 +77,4 @@ hipError_t launch_denoise(const float *img, const float *var, int W, int H, int 
 hipError_t launch_splat(const DevScene &S, const float4 *rec, const SplatDesc &sd, uint32_t nblocks, float *film,
                         Counters *C, hipStream_t st);
 
-bool trav_stats_take(unsigned long long out[8]);  // NORI_TRAV_STATS builds (diagnostic)
-// Scan-mode trace kernels: 1 k_trace_bin, 0 k_extend_scan / k_shadow_scan, 2
-// both, compared (NORI_EXTEND_CHECK=1); extend_check_take reads and resets
-// (hit mismatches, compared extension rays, occlusion mismatches, compared shadow rays).
-int extend_mode();
-bool ext_prof_take(unsigned long long out[4]);  // NORI_PROF_EXTEND builds (diagnostic)
-bool extend_check_take(unsigned long long out[4]);
 }  // namespace nori

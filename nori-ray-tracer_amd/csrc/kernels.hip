@@ -87,27 +87,8 @@ ND void load_node(const DevScene &S, uint32_t ref, float4 &mnx, float4 &mny, flo
     rf = gld(nd + 6);
 }
 
-// 1 / det of the triangle tests: rcp_rn (NORI_SCAN_RCP_UNCHECKED, a
-// measurement build: without rcp_rn's range branch -- not exact for
-// |det| > 2^125).
-ND float rcp_det(float x) {
-#if defined(NORI_SCAN_RCP_UNCHECKED) && defined(__HIP_DEVICE_COMPILE__)
-    const float r = __builtin_amdgcn_rcpf(x);
-    const float e = __builtin_fmaf(-x, r, 1.0f);
-    return __builtin_fmaf(e, r, r);
-#elif defined(NORI_RCP_WAVE) && defined(__HIP_DEVICE_COMPILE__)
-    // rcp_rn with its range test as one wave-uniform branch (no exec-mask
-    // save and restore around the common case)
-    const float r = __builtin_amdgcn_rcpf(x);
-    const float e = __builtin_fmaf(-x, r, 1.0f);
-    float q = __builtin_fmaf(e, r, r);
-    const bool in = __builtin_fabsf(x) <= 0x1p125f;
-    if (__builtin_expect(!__all(in), 0)) q = in ? q : 1.0f / x;
-    return q;
-#else
-    return rcp_rn(x);
-#endif
-}
+// 1 / det of the triangle tests, correctly rounded (== 1.0f / det, tools/rcp_check.hip).
+ND float rcp_det(float x) { return rcp_rn(x); }
 // Mesh::rayIntersect (mesh.cpp:83-120), edges precomputed exactly.
 ND bool tri_hit(const float4 &a, const float4 &b, const float4 &c, const TRay &r, float &t, float &u, float &v) {
     V3 v0 = ld3(a), e1 = ld3(b), e2 = ld3(c);
@@ -209,9 +190,6 @@ ND bool sphere_hit_nb(const float4 &a, const float4 &b, const TRay &r, float &t)
     return (disc > 0) && (h1 || h2);
 }
 
-#ifndef NORI_CAMERA_CULL
-#define NORI_CAMERA_CULL 1
-#endif
 // sphere_hit_nb with its square root and its two divisions in short
 // correctly rounded forms, so the same t bits for every ray: sqrt_rn's core
 // (v_sqrt_f32 and one Tuckerman test each way, exhaustively exact on
@@ -456,10 +434,7 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
         for (int k = 0; k < K; ++k) z = z || (live[k] && !(r[k].mint > 0.0f));
         gen = __any(z);
     }
-#ifndef NORI_SCAN_SKIP  // measurement builds only: 1 skips the axis-plane pairs, 2 the other triangles, 4 the spheres
-#define NORI_SCAN_SKIP 0
-#endif
-    if ((NORI_SCAN_SKIP & 1) == 0 && NORI_SC_PLANE_END(2) && !gen) {
+    if (NORI_SC_PLANE_END(2) && !gen) {
         scan_planes<0, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<1, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
         scan_planes<2, K, ANY, CULL>(S, r, live, tb, pb, lb, ub, vb, found);
@@ -470,7 +445,7 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
     }
     const uint32_t nt = NORI_SC_TRIS, n = NORI_SC_PRIMS, real = NORI_SC_REAL;
     NORI_SC_UNROLL
-    for (uint32_t i = 2 * NORI_SC_PLANE_END(2); (NORI_SCAN_SKIP & 2) == 0 && i < nt; i += kScanGroup) {
+    for (uint32_t i = 2 * NORI_SC_PLANE_END(2); i < nt; i += kScanGroup) {
         if (ANY && all_done()) return;
         float4 q[3 * kScanGroup];
 #pragma unroll
@@ -481,7 +456,7 @@ ND void scan_core(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
                 scan_tri<K, ANY>(q[3 * g], q[3 * g + 1], q[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
     }
     NORI_SC_UNROLL
-    for (uint32_t i = nt; (NORI_SCAN_SKIP & 4) == 0 && i < n; ++i) {
+    for (uint32_t i = nt; i < n; ++i) {
         if (ANY && all_done()) return;
         const float4 p0 = NORI_SC_PRIM(3 * i), p1 = NORI_SC_PRIM(3 * i + 1);
         const uint32_t pos = __float_as_uint(NORI_SC_PRIM(3 * i + 2).w);
@@ -518,18 +493,6 @@ ND void scan_rays(const DevScene &S, TRay (&r)[K], bool (&live)[K], float (&tb)[
 #define NORI_LEAF_BATCH 1
 #endif
 constexpr int kLeafBatch = NORI_LEAF_BATCH;
-
-// NORI_TRAV_STATS builds (diagnostic): per-ray counts of the BVH walks of
-// k_extend / k_shadow -- inner nodes fetched, leaves entered, primitives
-// tested, rays -- summed over the launches (nori_trav_stats).
-#ifdef NORI_TRAV_STATS
-// (one copy per translation unit: the reader sees unit 0's kernels, i.e.
-// k_extend / k_shadow / k_trace, not the tail finisher)
-static __device__ unsigned long long g_trav_stats[8];
-#define NORI_TSTAT(k, n) (tstat[k] += (n))
-#else
-#define NORI_TSTAT(k, n)
-#endif
 
 // LDS words per lane of a traversal stack of depth STACK: child refs and entry distances.
 // (stack_lds_entries(STACK) entries: the LDS budget stays STACK words, so the
@@ -582,27 +545,8 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     uint32_t ref = 0;
     int sp = 0;
     bool found = false;
-#ifdef NORI_TRAV_STATS
-    uint32_t tstat[3] = {0, 0, 0};
-    struct Flush {
-        uint32_t *t;
-        ND ~Flush() {  // per lane (lanes leave the walk at different points)
-            atomicAdd(&g_trav_stats[0], (unsigned long long)t[0]);
-            atomicAdd(&g_trav_stats[1], (unsigned long long)t[1]);
-            atomicAdd(&g_trav_stats[2], (unsigned long long)t[2]);
-            atomicAdd(&g_trav_stats[3], 1ull);
-            const uint32_t v = t[0] + t[1];  // node + leaf visits of this ray
-            atomicMax(&g_trav_stats[4], (unsigned long long)v);
-            if (v > 64) {
-                atomicAdd(&g_trav_stats[5], 1ull);
-                atomicAdd(&g_trav_stats[6], (unsigned long long)v);
-            }
-        }
-    } flush{tstat};
-#endif
     for (;;) {
         if (!(ref & 0x80000000u)) {
-            NORI_TSTAT(0, 1);
             float4 mnx, mny, mnz, mxx, mxy, mxz, rf;
             load_node(S, ref, mnx, mny, mnz, mxx, mxy, mxz, rf);
             float k0, k1, k2, k3;
@@ -655,8 +599,6 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
             // record) -- one memory round trip per batch instead of one or
             // two per primitive.  Tested in leaf order, as bvh.cpp:440-452.
             const uint32_t start = ref & 0x1FFFFFFu, end = start + ((ref >> 25) & 63u) + 1u;
-            NORI_TSTAT(1, 1);
-            NORI_TSTAT(2, end - start);
             for (uint32_t i0 = start; i0 < end; i0 += kLeafBatch) {
                 float4 q[kLeafBatch][3];
 #pragma unroll
@@ -727,7 +669,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 
         bool live[1] = {true}, found[1];
         float t1[1], u1[1], v1[1];
         uint32_t p1[1];
-        scan_rays<1, ANY, 1, true>(S, rr, live, t1, p1, u1, v1, found);
+        // S.trace_cull: the scan's wall-pair skips under test (wave-uniform)
+        if (S.trace_cull == 2) scan_rays<1, ANY, 2, true>(S, rr, live, t1, p1, u1, v1, found);
+        else if (S.trace_cull == 0) scan_rays<1, ANY, 0, true>(S, rr, live, t1, p1, u1, v1, found);
+        else scan_rays<1, ANY, 1, true>(S, rr, live, t1, p1, u1, v1, found);
         t = t1[0], p = p1[0], u = u1[0], v = v1[0], h = found[0];
     } else {
         h = traverse<STACK, ANY>(S, r, stk + threadIdx.x, t, p, u, v);
@@ -736,51 +681,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 
     else hits[q] = make_float4(t, __uint_as_float(p), u, v);
 }
 
-// Trace work-groups are dealt out over groups of kTraceGroup consecutive
-// segments: the queue entries of a group are numbered through a prefix over
-// its segment counts and work-group j of the group takes entries
-// [128j, 128j+128).  Partly filled segments (a segment's shadow queue is about
-// half full; the drain phase empties them) therefore do not leave waves
-// partly idle, and every thread still traces one ray (short-lived waves keep
-// the kernel's tail short).
-struct SegRange {
-    uint32_t pre[kTraceGroup + 1];
-    uint32_t s0;
-};
-constexpr uint32_t kTraceSlices = kTraceGroup * kSeg / kTraceBlock;  // work-groups per group
-ND SegRange seg_range(const uint32_t *cnt, uint32_t G, uint32_t bid) {
-    SegRange r;
-    r.s0 = (bid / kTraceSlices) * kTraceGroup;
-    r.pre[0] = 0;
-#pragma unroll
-    for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
-    return r;
-}
-ND SegRange seg_range_k(const uint32_t *cnt, uint32_t G, uint32_t K) {
-    SegRange r;
-    r.s0 = (blockIdx.x / (kTraceSlices / K)) * kTraceGroup;
-    r.pre[0] = 0;
-#pragma unroll
-    for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
-    return r;
-}
-ND SegRange seg_range_per(const uint32_t *cnt, uint32_t G, uint32_t per) {  // `per` work-groups per group
-    SegRange r;
-    r.s0 = (blockIdx.x / per) * kTraceGroup;
-    r.pre[0] = 0;
-#pragma unroll
-    for (int k = 0; k < kTraceGroup; ++k) r.pre[k + 1] = r.pre[k] + (r.s0 + k < G ? cnt[r.s0 + k] : 0u);
-    return r;
-}
-ND uint32_t seg_entry(const SegRange &r, uint32_t i) {
-    uint32_t k = 0;
-#pragma unroll
-    for (int j = 1; j < kTraceGroup; ++j) k += i >= r.pre[j] ? 1u : 0u;
-    uint32_t base = r.pre[0];
-#pragma unroll
-    for (int j = 1; j < kTraceGroup; ++j) base = k == (uint32_t)j ? r.pre[j] : base;
-    return (r.s0 + k) * kSeg + (i - base);
-}
+// Entry numbering of the trace launches: seg_index.h.
+constexpr uint32_t kTraceSlices = kTraceGroup * kSeg / kTraceBlock;  // BVH-walk work-groups per group
+ND SegRange seg_range(const uint32_t *cnt, uint32_t G, uint32_t bid) { return seg_group(cnt, G, bid, kTraceSlices); }
 
 // A path queue entry's ray (dev_scene.h PathQueue): camera rays carry 1/z of
 // their camera-space direction (mint = nearClip/z, maxt = farClip/z, as
@@ -799,7 +702,7 @@ template <int STACK>
 ND void extend_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt, uint32_t G, uint32_t bid,
                     uint32_t *stk) {
     const SegRange sr = seg_range(cnt, G, bid);
-    const uint32_t i = (bid % kTraceSlices) * kTraceBlock + threadIdx.x;
+    const uint32_t i = seg_first(bid, kTraceSlices, kTraceBlock, 1, threadIdx.x);
     if (i < sr.pre[kTraceGroup]) {
         const uint32_t q = seg_entry(sr, i);
         TRay r;
@@ -828,7 +731,7 @@ template <int STACK>
 ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                     uint32_t bid, uint32_t *stk) {
     const SegRange sr = seg_range(shcnt, G, bid);
-    const uint32_t i = (bid % kTraceSlices) * kTraceBlock + threadIdx.x;
+    const uint32_t i = seg_first(bid, kTraceSlices, kTraceBlock, 1, threadIdx.x);
     if (i < sr.pre[kTraceGroup]) {
         const uint32_t q = seg_entry(sr, i);
         float4 a = sq.ray_o[q], b = sq.ray_d[q];
@@ -873,9 +776,6 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
-#ifdef NORI_PROF_EXTEND
-static __device__ unsigned long long g_ext_prof[4];  // per wave: loads, scan, store clocks; waves
-#endif
 // Work-group sizes of the scan-mode extension and shadow kernels: 256
 // threads (C2 median 5176 against 5023 Msamples/s with 128; 512 makes the
 // extension launch slower, 0.0786 against 0.0752 ms).
@@ -886,7 +786,11 @@ static __device__ unsigned long long g_ext_prof[4];  // per wave: loads, scan, s
 #define NORI_SHADOW_BLOCK 256
 #endif
 template <int K, uint32_t B>
-constexpr uint32_t scan_per() { return kTraceGroup * kSeg / (B * K); }  // work-groups per group
+constexpr uint32_t scan_per() {  // work-groups per group of kTraceGroup segments
+    static_assert(K >= 1 && kTraceGroup * kSeg % (B * K) == 0 && kTraceGroup * kSeg / (B * K) >= 1,
+                  "a scan work-group of B threads x K rays must tile the group's kTraceGroup * kSeg entries");
+    return kTraceGroup * kSeg / (B * K);
+}
 #ifdef NORI_EXTEND_WAVES  // tuning: waves per SIMD the register allocation must allow
 #define NORI_EXTEND_ATTR __attribute__((amdgpu_waves_per_eu(NORI_EXTEND_WAVES)))
 #else
@@ -895,20 +799,17 @@ constexpr uint32_t scan_per() { return kTraceGroup * kSeg / (B * K); }  // work-
 template <int K>
 __global__ __launch_bounds__(NORI_EXTEND_BLOCK) NORI_EXTEND_ATTR void k_extend_scan(DevScene S, PathQueue pq,
                                                                                  const uint32_t *cnt, uint32_t G) {
-    const SegRange sr = seg_range_per(cnt, G, scan_per<K, NORI_EXTEND_BLOCK>());
+    const SegRange sr = seg_group(cnt, G, blockIdx.x, scan_per<K, NORI_EXTEND_BLOCK>());
     // a lane's K rays are entries NORI_EXTEND_BLOCK apart (adjacent entries, so
     // that a wave covers 64 K consecutive ones, measured 1 % slower)
     constexpr uint32_t STEP = NORI_EXTEND_BLOCK;
-    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % scan_per<K, NORI_EXTEND_BLOCK>()) * NORI_EXTEND_BLOCK * K + threadIdx.x;
+    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(blockIdx.x, scan_per<K, NORI_EXTEND_BLOCK>(), NORI_EXTEND_BLOCK, K, threadIdx.x);
     if (i0 >= n) return;  // entries fill the slice from its start
     TRay r[K];
     bool live[K];
     uint32_t q[K];
     // lanes past the end load entry i0 again (unconditional loads: no
     // branch, so all of them are in flight together)
-#ifdef NORI_PROF_EXTEND  // diagnostic build: shader clocks of the wave's phases (ext_prof_take)
-    const uint64_t c0 = __builtin_amdgcn_s_memtime();
-#endif
     bool cam = true;  // every live ray of this lane a camera ray
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -927,40 +828,18 @@ __global__ __launch_bounds__(NORI_EXTEND_BLOCK) NORI_EXTEND_ATTR void k_extend_s
     // in-plane filter skips the other pairs for the whole wave.  The
     // incoherent waves of bounce rays test every pair unchecked (a wave-wide
     // skip never happens there; NORI_CAMERA_CULL=0 tests every wave so).
-#ifdef NORI_PROF_EXTEND
-    {  // wait for the ray loads: the first use of every loaded word
-        float z = 0.0f;
-#pragma unroll
-        for (int k = 0; k < K; ++k) z += r[k].o.x + r[k].o.y + r[k].o.z + r[k].d.x + r[k].d.y + r[k].d.z + r[k].mint;
-        if (__builtin_isnan(z) && threadIdx.x == 1000) r[0].mint = z;
-    }
-    const uint64_t c1 = __builtin_amdgcn_s_memtime();
-#endif
-    if (NORI_CAMERA_CULL && S.plane_f && __all(cam)) scan_rays<K, false, 2>(S, r, live, t, p, u, v, f);
+    if (S.camera_cull && S.plane_f && __all(cam)) scan_rays<K, false, 2>(S, r, live, t, p, u, v, f);
     else scan_rays<K, false, 0>(S, r, live, t, p, u, v, f);
-#ifdef NORI_PROF_EXTEND
-    const uint64_t c2 = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (i0 + k * STEP < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
-#ifdef NORI_PROF_EXTEND
-    __builtin_amdgcn_s_waitcnt(0);  // the stores' completion
-    const uint64_t c3 = __builtin_amdgcn_s_memtime();
-    if (lane_id() == 0) {
-        atomicAdd(&g_ext_prof[0], (unsigned long long)(c1 - c0));
-        atomicAdd(&g_ext_prof[1], (unsigned long long)(c2 - c1));
-        atomicAdd(&g_ext_prof[2], (unsigned long long)(c3 - c2));
-        atomicAdd(&g_ext_prof[3], 1ull);
-    }
-#endif
 }
 
 template <int K>
 __global__ __launch_bounds__(NORI_SHADOW_BLOCK) void k_shadow_scan(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
                                                             float4 *rec, uint32_t G) {
-    const SegRange sr = seg_range_per(shcnt, G, scan_per<K, NORI_SHADOW_BLOCK>());
-    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % scan_per<K, NORI_SHADOW_BLOCK>()) * NORI_SHADOW_BLOCK * K + threadIdx.x;
+    const SegRange sr = seg_group(shcnt, G, blockIdx.x, scan_per<K, NORI_SHADOW_BLOCK>());
+    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(blockIdx.x, scan_per<K, NORI_SHADOW_BLOCK>(), NORI_SHADOW_BLOCK, K, threadIdx.x);
     if (i0 >= n) return;
     TRay r[K];
     bool live[K], valid[K];
@@ -988,300 +867,6 @@ __global__ __launch_bounds__(NORI_SHADOW_BLOCK) void k_shadow_scan(DevScene S, S
     for (int k = 0; k < K; ++k)
         if (valid[k] && !f[k]) shadow_add(rec, c[k]);
 }
-
-// ------------------------------------------------------------------ binned extension scan
-// k_extend_scan tests every axis-plane pair and every sphere against every
-// ray; a ray inside the Cornell box can be accepted by one wall (where it
-// leaves the box) and passes near a sphere rarely, so most of those tests are
-// wasted, yet a 64-ray wave always holds some ray for every wall.
-// k_extend_bin therefore moves those tests out of the ray's lane: (1) every
-// lane filters its ray against each pair -- a dozen VALU instructions
-// (pair_candidate, exact: runtime.hip plane_filters) -- and each sphere --
-// the reference's own discriminant, disc > 0 being the sphere test's first
-// condition -- and hands the (ray, pair) and (ray, sphere) candidates to two
-// work-group lists in LDS, while it scans the remaining triangles itself as
-// before; (2) the work-group's four waves run the listed candidates 64 at a
-// time, pairs first, then spheres, each lane one candidate with the records
-// and the ray read from LDS -- dense lanes whatever ray they belong to; (3)
-// every lane merges its candidates' results into its own closest hit.  The
-// tie rule of scan_core (closest t, then the later leaf position) makes the
-// result independent of the order of the tests, so the hits are those of
-// k_extend_scan bit for bit (NORI_EXTEND_CHECK compares the two on every
-// launch).  A ray with more than kBinSlots candidates tests everything in its
-// own lane.
-#ifndef NORI_EXTEND_BIN
-#define NORI_EXTEND_BIN 0
-#endif
-#ifndef NORI_BIN_SPHERES
-#define NORI_BIN_SPHERES 1
-#endif
-#ifndef NORI_SHADOW_BIN
-#define NORI_SHADOW_BIN 1
-#endif
-constexpr int kBinBlock = 256;
-constexpr uint32_t kBinSlices = kTraceGroup * kSeg / kBinBlock;  // work-groups per group of segments
-constexpr int kBinSlots = 3;
-constexpr uint32_t kBinMaxRec = 64;  // staged records: the pairs' (2 per pair) and the spheres'
-// A ray's candidates: count and up to kBinSlots entries of 8 bits (kind << 7
-// | index: kind 0 a pair, 1 a sphere), 8 bits apart.
-struct BinCand {
-    uint32_t n = 0, e = 0;
-    ND void add(uint32_t v) {
-        e = n < (uint32_t)kBinSlots ? (e | v << (8 * n)) : e;
-        ++n;
-    }
-};
-template <int A>
-ND void bin_axis(const DevScene &S, const TRay &r, bool live, float mlo, float mhi, BinCand &bc) {
-    constexpr int B = (A + 1) % 3, C = (A + 2) % 3;
-    const uint32_t g0 = A == 0 ? 0u : S.plane_end[A - 1], g1 = S.plane_end[A];
-    if (g0 == g1) return;
-    const float so = fabsf(comp<B>(r.o)) + fabsf(comp<C>(r.o)), sd = fabsf(comp<B>(r.d)) + fabsf(comp<C>(r.d));
-    for (uint32_t g = g0; g < g1; ++g) {
-        const float4 f0 = S.plane_f[2 * g], f1 = S.plane_f[2 * g + 1];
-        if (live && pair_candidate<A>(r, f0, f1, mlo, mhi, so, sd)) bc.add(g);
-    }
-}
-// The discriminant of Sphere::rayIntersect (sphere.cpp:43-76) exactly as
-// sphere_hit_nb computes it: disc > 0 is the test's first condition.
-ND float sphere_disc(const float4 &a, const float4 &b, const TRay &r) {
-    V3 oc = r.o - ld3(a);
-    float rad = b.x;
-    float A = dot(r.d, r.d);
-    float B = 2.0f * dot(oc, r.d);
-    float C = dot(oc, oc) - rad * rad;
-    return B * B - 4 * A * C;
-}
-
-#if NORI_TU == 0
-// ANY = false: closest hit of the path queue's extension rays (k_extend_scan's
-// results).  ANY = true: the shadow queue's rays, any hit; an unoccluded ray
-// adds its payload to its sample record (k_shadow_scan), or with FLAGS its
-// occlusion to flags[entry] (NORI_EXTEND_CHECK).
-template <bool ANY, bool FLAGS>
-__global__ __launch_bounds__(kBinBlock) void k_trace_bin(DevScene S, PathQueue pq, ShadowQueue sq, const uint32_t *cnt,
-                                                         uint32_t G, float4 *rec, uint32_t *flags) {
-    constexpr uint32_t NW = kBinBlock / 64, CAP = 64 * kBinSlots;
-    __shared__ float4 s_ray[2][kBinBlock];              // (o, mint), (d, maxt)
-    __shared__ float4 s_res[kBinSlots][kBinBlock];      // per (slot, ray): t, u, v, prim | pos << 16
-    __shared__ float4 s_rec[3 * kBinMaxRec];            // the pairs' records, then the spheres'
-    __shared__ uint16_t s_item[2][NW][CAP];             // per kind and wave: ray | index << 8 | slot << 14
-    __shared__ uint32_t s_nitem[2][NW];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const SegRange sr = seg_range_k(cnt, G, kTraceSlices / kBinSlices);
-    const uint32_t n = sr.pre[kTraceGroup], i0 = (blockIdx.x % kBinSlices) * kBinBlock, i = i0 + tid;
-    if (i0 >= n) return;  // the whole work-group: its slice is empty
-    const uint32_t np = S.plane_end[2], nt = S.num_scan_tris, nall = S.num_prims;
-    const uint32_t ns = NORI_BIN_SPHERES ? nall - nt : 0u, sph0 = 6 * np;
-    for (uint32_t j = tid; j < 6 * np; j += kBinBlock) s_rec[j] = S.prims[j];
-    for (uint32_t j = tid; j < 3 * ns; j += kBinBlock) s_rec[sph0 + j] = S.prims[3 * nt + j];
-    const bool valid = i < n;
-    const uint32_t q = seg_entry(sr, valid ? i : i0);
-    TRay r[1];
-    bool live[1] = {valid};
-    float4 pay = make_float4(0, 0, 0, 0);
-    if constexpr (ANY) {
-        const float4 a = sq.ray_o[q], b = sq.ray_d[q];
-        if (!FLAGS) pay = sq.payload[q];  // fetched now: its latency hides behind the tests
-        r[0].o = ld3(a);
-        r[0].d = ld3(b);
-        r[0].mint = a.w;
-        r[0].maxt = b.w;
-    } else {
-        path_ray(S, pq.ray_o[q], pq.ray_d[q], r[0]);
-    }
-    scan_prologue<1>(S, r, live);
-    float tb[1] = {INF_F}, ub[1] = {0.0f}, vb[1] = {0.0f};
-    uint32_t pb[1] = {0xFFFFFFFFu}, lb[1] = {0u};
-    bool found[1] = {false};
-    // the ray's own tests of the triangles outside the pairs (scan_core's
-    // loop); a closest-hit ray's maxt shrinks to its hit, so farther
-    // candidates are not handed out; an occluded shadow ray hands out none
-    for (uint32_t k = 2 * np; k < nt; k += kScanGroup) {
-        if (ANY && !__any(live[0] && !found[0])) break;
-        const float4 *p = S.prims + 3 * (size_t)k;
-        float4 qq[3 * kScanGroup];
-#pragma unroll
-        for (uint32_t j = 0; j < 3 * kScanGroup; ++j) qq[j] = p[j];
-#pragma unroll
-        for (uint32_t g = 0; g < kScanGroup; ++g)
-            if (k + g < S.num_scan_real)  // (the padding records never hit)
-                scan_tri<1, ANY>(qq[3 * g], qq[3 * g + 1], qq[3 * g + 2], r, live, tb, pb, lb, ub, vb, found);
-    }
-    const bool open = live[0] && !(ANY && found[0]);
-    // (1) candidates
-    BinCand bc;
-    {
-        const float mlo = r[0].mint > 0.0f ? r[0].mint * kPlaneLo : -INF_F;
-        const float mhi = r[0].maxt > 0.0f ? r[0].maxt * kPlaneHi : INF_F;
-        bin_axis<0>(S, r[0], open, mlo, mhi, bc);
-        bin_axis<1>(S, r[0], open, mlo, mhi, bc);
-        bin_axis<2>(S, r[0], open, mlo, mhi, bc);
-    }
-    for (uint32_t k = 0; k < ns; ++k) {
-        const float4 *p = S.prims + 3 * (size_t)(nt + k);
-        if (open && sphere_disc(p[0], p[1], r[0]) > 0.0f) bc.add(128u | k);
-    }
-    const bool dense = bc.n > (uint32_t)kBinSlots;
-    const uint32_t m = dense ? 0u : bc.n;
-    s_ray[0][tid] = make_float4(r[0].o.x, r[0].o.y, r[0].o.z, r[0].mint);
-    s_ray[1][tid] = make_float4(r[0].d.x, r[0].d.y, r[0].d.z, r[0].maxt);
-#pragma unroll
-    for (uint32_t kind = 0; kind < 2; ++kind) {
-        uint32_t mk = 0;
-#pragma unroll
-        for (int e = 0; e < kBinSlots; ++e) mk += ((uint32_t)e < m && ((bc.e >> (8 * e + 7)) & 1u) == kind) ? 1u : 0u;
-        const uint64_t b1 = __ballot(mk >= 1u), b2 = __ballot(mk >= 2u), b3 = __ballot(mk >= 3u);
-        uint32_t at = rank_in(b1) + rank_in(b2) + rank_in(b3);
-#pragma unroll
-        for (int e = 0; e < kBinSlots; ++e) {
-            const uint32_t v = (bc.e >> (8 * e)) & 255u;
-            if ((uint32_t)e < m && (v >> 7) == kind) s_item[kind][w][at++] = (uint16_t)(tid | (v & 63u) << 8 | (uint32_t)e << 14);
-        }
-        if (lane == 0) s_nitem[kind][w] = (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
-    }
-    // a dense ray tests every pair and sphere itself
-    auto sphere_own = [&](uint32_t k, bool on) {
-        const float4 *p = S.prims + 3 * (size_t)k;
-        const float4 p0 = p[0], p1 = p[1];
-        const uint32_t pos = __float_as_uint(p[2].w);
-        float t = 0;
-        const bool h = sphere_hit_nb(p0, p1, r[0], t);  // t <= r.maxt = tb
-        if (h && on && (ANY || t != tb[0] || pos > lb[0])) {
-            found[0] = true;
-            if (!ANY) {
-                r[0].maxt = tb[0] = t;
-                ub[0] = vb[0] = 0.0f;
-                pb[0] = __float_as_uint(p0.w);
-                lb[0] = pos;
-            }
-        }
-    };
-    if (__any(dense)) {
-        bool dl[1] = {dense && open};
-        scan_planes<0, 1, ANY, ANY>(S, r, dl, tb, pb, lb, ub, vb, found);
-        scan_planes<1, 1, ANY, ANY>(S, r, dl, tb, pb, lb, ub, vb, found);
-        scan_planes<2, 1, ANY, ANY>(S, r, dl, tb, pb, lb, ub, vb, found);
-        for (uint32_t k = nt; k < nt + ns; ++k) sphere_own(k, dl[0]);
-    }
-    for (uint32_t k = nt + ns; k < nall; ++k) sphere_own(k, live[0]);  // (NORI_BIN_SPHERES=0)
-    __syncthreads();
-    // (2) the work-group's candidates, 64 per wave and round: pairs, then spheres
-    {
-        uint32_t pre[2][NW + 1];
-#pragma unroll
-        for (int kind = 0; kind < 2; ++kind) {
-            pre[kind][0] = 0;
-#pragma unroll
-            for (uint32_t v = 0; v < NW; ++v) pre[kind][v + 1] = pre[kind][v] + s_nitem[kind][v];
-        }
-        const uint32_t nc0 = (pre[0][NW] + 63u) / 64u, nch = nc0 + (pre[1][NW] + 63u) / 64u;
-        for (uint32_t c = w; c < nch; c += NW) {
-            const uint32_t kind = c < nc0 ? 0u : 1u, j = (kind ? c - nc0 : c) * 64u + lane;
-            if (j >= pre[kind][NW]) continue;
-            uint32_t k = 0;
-#pragma unroll
-            for (uint32_t v = 1; v < NW; ++v) k += j >= pre[kind][v] ? 1u : 0u;
-            uint32_t base = 0;
-#pragma unroll
-            for (uint32_t v = 1; v < NW; ++v) base = k == v ? pre[kind][v] : base;
-            const uint32_t item = s_item[kind][k][j - base];
-            const uint32_t rid = item & 255u, idx = (item >> 8) & 63u, slot = item >> 14;
-            const float4 ro = s_ray[0][rid], rd = s_ray[1][rid];
-            TRay x;
-            x.o = ld3(ro);
-            x.mint = ro.w;
-            x.d = ld3(rd);
-            x.maxt = rd.w;
-            float4 res = make_float4(INF_F, 0.0f, 0.0f, 0.0f);
-            if (kind == 0) {
-                const float4 *p = s_rec + 6 * idx;
-                uint32_t lpos = 0u;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const float4 a = p[3 * e], b = p[3 * e + 1], c = p[3 * e + 2];
-                    float t = 0, u = 0, v = 0;
-                    const uint32_t pos = __float_as_uint(c.w);
-                    if (tri_hit_nb(a, b, c, x, t, u, v) && (ANY || t != res.x || pos > lpos)) {
-                        res = ANY ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
-                                  : make_float4(t, u, v, __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | pos << 16));
-                        if (!ANY) x.maxt = t;
-                        lpos = pos;
-                    }
-                }
-            } else {
-                const float4 *p = s_rec + sph0 + 3 * idx;
-                const float4 a = p[0];
-                float t = 0;
-                if (sphere_hit_nb(a, p[1], x, t))
-                    res = ANY ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
-                              : make_float4(t, 0.0f, 0.0f,
-                                            __uint_as_float((__float_as_uint(a.w) & 0xFFFFu) | __float_as_uint(p[2].w) << 16));
-            }
-            s_res[slot][rid] = res;
-        }
-    }
-    __syncthreads();
-    // (3) merge
-#pragma unroll
-    for (int e = 0; e < kBinSlots; ++e) {
-        if ((uint32_t)e < m) {
-            const float4 res = s_res[e][tid];
-            const uint32_t wd = __float_as_uint(res.w), pos = wd >> 16;
-            if (ANY) {
-                found[0] = found[0] || res.x == 0.0f;
-            } else if (res.x < tb[0] || (res.x == tb[0] && pos > lb[0])) {
-                tb[0] = res.x;
-                ub[0] = res.y;
-                vb[0] = res.z;
-                pb[0] = wd & 0xFFFFu;
-                lb[0] = pos;
-            }
-        }
-    }
-    if (!valid) return;
-    if constexpr (!ANY) pq.hit[q] = make_float4(tb[0], __uint_as_float(pb[0]), ub[0], vb[0]);
-    else if constexpr (FLAGS) flags[q] = found[0] ? 1u : 0u;
-    else if (!found[0]) shadow_add(rec, pay);
-}
-
-// NORI_EXTEND_CHECK (diagnostic): mismatching hit records between the two
-// extension kernels on the same queue (t and prim bitwise, u and v as values),
-// and mismatching occlusion between the two shadow kernels.
-__device__ unsigned long long g_extend_check[4];
-__global__ __launch_bounds__(kTraceBlock) void k_extend_cmp(const float4 *a, const float4 *b, const uint32_t *cnt,
-                                                            uint32_t G) {
-    const uint32_t e = blockIdx.x * kTraceBlock + threadIdx.x, s = e / kSeg;
-    if (s >= G || e % kSeg >= cnt[s]) return;
-    const float4 x = a[e], y = b[e];
-    const bool same = __float_as_uint(x.x) == __float_as_uint(y.x) && __float_as_uint(x.y) == __float_as_uint(y.y) &&
-                      x.z == y.z && x.w == y.w;
-    atomicAdd(&g_extend_check[1], 1ull);
-    if (!same) atomicAdd(&g_extend_check[0], 1ull);
-}
-// the occlusion k_shadow_scan finds for every shadow ray (scan_rays, one ray
-// per thread), compared with k_trace_bin<true, true>'s flags
-__global__ __launch_bounds__(kTraceBlock) void k_shadow_cmp(DevScene S, ShadowQueue sq, const uint32_t *cnt, uint32_t G,
-                                                            const uint32_t *flags) {
-    const uint32_t e = blockIdx.x * kTraceBlock + threadIdx.x, s = e / kSeg;
-    const bool ok = s < G && e % kSeg < cnt[s < G ? s : 0];
-    if (!__any(ok)) return;
-    const uint32_t q = ok ? e : (s < G ? s * kSeg : 0u);
-    const float4 a = sq.ray_o[q], b = sq.ray_d[q];
-    TRay r[1];
-    r[0].o = ld3(a);
-    r[0].d = ld3(b);
-    r[0].mint = a.w;
-    r[0].maxt = b.w;
-    bool live[1] = {ok}, f[1];
-    float t[1], u[1], v[1];
-    uint32_t p[1];
-    scan_rays<1, true>(S, r, live, t, p, u, v, f);
-    if (!ok) return;
-    atomicAdd(&g_extend_check[3], 1ull);
-    if ((flags[q] != 0u) != f[0]) atomicAdd(&g_extend_check[2], 1ull);
-}
-#endif
 
 // ------------------------------------------------------------------ shading helpers
 struct SurfHit {
@@ -3185,52 +2770,12 @@ hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue 
 
 #endif
 #if NORI_TU == 0
-// The binned kernels need every staged record in kBinMaxRec.
-static bool bin_ok(const DevScene &S) {
-    return S.plane_f && 2 * S.plane_end[2] + (S.num_prims - S.num_scan_tris) <= kBinMaxRec;
-}
-// Shadow rays through k_trace_bin<true> (NORI_SHADOW_BIN=0: k_shadow_scan).
-static bool shadow_bin() {
-    static const bool on = [] {
-        const char *e = std::getenv("NORI_SHADOW_BIN");
-        return e ? e[0] != '0' : NORI_SHADOW_BIN != 0;
-    }();
-    return on;
-}
-// Diagnostic scratch of NORI_EXTEND_CHECK (grown as needed, never freed).
-static float4 *check_scratch(size_t bytes) {
-    static float4 *p = nullptr;
-    static size_t have = 0;
-    if (have < bytes) {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        have = 0;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-        have = bytes;
-    }
-    return p;
-}
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st) {
-    dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
+    dim3 g(seg_grid(G, kTraceSlices)), b(kTraceBlock);
     if (stack == 0) {
-        const dim3 gk((G + kTraceGroup - 1) / kTraceGroup * scan_per<kScanRays, NORI_EXTEND_BLOCK>()), bk(NORI_EXTEND_BLOCK);
-        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
-        const int mode = extend_mode();
-        const ShadowQueue nsq{nullptr, nullptr, nullptr};
-        if (mode == 1 && bin_ok(S)) {
-            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q, nsq, cnt, G, nullptr, nullptr);
-            return hipGetLastError();
-        }
+        const dim3 gk(seg_grid(G, scan_per<kScanRays, NORI_EXTEND_BLOCK>())), bk(NORI_EXTEND_BLOCK);
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
-        if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK
-            float4 *scratch = check_scratch((size_t)G * kSeg * sizeof(float4));
-            if (!scratch) return hipErrorOutOfMemory;
-            PathQueue q2 = q;
-            q2.hit = scratch;
-            hipLaunchKernelGGL((k_trace_bin<false, false>), gb, bb, 0, st, S, q2, nsq, cnt, G, nullptr, nullptr);
-            hipLaunchKernelGGL(k_extend_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, q.hit, scratch, cnt, G);
-        }
         return hipGetLastError();
     }
     switch (stack) {
@@ -3244,22 +2789,9 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
 
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st) {
-    dim3 g((G + kTraceGroup - 1) / kTraceGroup * kTraceSlices), b(kTraceBlock);
+    dim3 g(seg_grid(G, kTraceSlices)), b(kTraceBlock);
     if (stack == 0) {
-        const dim3 gk((G + kTraceGroup - 1) / kTraceGroup * scan_per<kScanRaysShadow, NORI_SHADOW_BLOCK>()), bk(NORI_SHADOW_BLOCK);
-        const dim3 gb((G + kTraceGroup - 1) / kTraceGroup * kBinSlices), bb(kBinBlock);
-        const int mode = extend_mode();
-        const PathQueue npq{nullptr, nullptr, nullptr, nullptr, nullptr};
-        if (mode == 1 && bin_ok(S) && shadow_bin()) {
-            hipLaunchKernelGGL((k_trace_bin<true, false>), gb, bb, 0, st, S, npq, sq, shcnt, G, rec, nullptr);
-            return hipGetLastError();
-        }
-        if (mode == 2 && bin_ok(S)) {  // NORI_EXTEND_CHECK: the occlusion of both kernels, before the record update
-            uint32_t *flags = reinterpret_cast<uint32_t *>(check_scratch((size_t)G * kSeg * sizeof(float4)));
-            if (!flags) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL((k_trace_bin<true, true>), gb, bb, 0, st, S, npq, sq, shcnt, G, nullptr, flags);
-            hipLaunchKernelGGL(k_shadow_cmp, dim3((uint32_t)((size_t)G * kSeg / kTraceBlock)), b, 0, st, S, sq, shcnt, G, flags);
-        }
+        const dim3 gk(seg_grid(G, scan_per<kScanRaysShadow, NORI_SHADOW_BLOCK>())), bk(NORI_SHADOW_BLOCK);
         hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, bk, 0, st, S, sq, shcnt, rec, G);
         return hipGetLastError();
     }
@@ -3367,50 +2899,6 @@ hipError_t launch_direct(const DevScene &S, const WorkDesc &wd, float4 *rec, Cou
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
-}
-
-// The scan-mode trace kernels: 1 k_trace_bin (default), 0 k_extend_scan / k_shadow_scan
-// (NORI_EXTEND_BIN=0), 2 both on every launch, compared (NORI_EXTEND_CHECK=1).
-int extend_mode() {
-    static const int mode = [] {
-        const char *c = std::getenv("NORI_EXTEND_CHECK");
-        if (c && c[0] == '1') return 2;
-        const char *e = std::getenv("NORI_EXTEND_BIN");
-        if (e) return e[0] == '0' ? 0 : 1;
-        return NORI_EXTEND_BIN ? 1 : 0;
-    }();
-    return mode;
-}
-// NORI_EXTEND_CHECK: read (and reset) the mismatch and compared-entry counts.
-bool extend_check_take(unsigned long long out[4]) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_extend_check), 4 * sizeof(unsigned long long)) != hipSuccess)
-        return false;
-    unsigned long long z[4] = {0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_extend_check), z, sizeof(z)) == hipSuccess;
-}
-
-// NORI_PROF_EXTEND builds: read (and reset) k_extend_scan's phase clocks; false otherwise.
-bool ext_prof_take(unsigned long long out[4]) {
-#ifdef NORI_PROF_EXTEND
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ext_prof), 4 * sizeof(unsigned long long)) != hipSuccess) return false;
-    unsigned long long z[4] = {0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_ext_prof), z, sizeof(z)) == hipSuccess;
-#else
-    (void)out;
-    return false;
-#endif
-}
-// NORI_TRAV_STATS builds: read (and reset) the BVH walk counters; false otherwise.
-bool trav_stats_take(unsigned long long out[8]) {
-#ifdef NORI_TRAV_STATS
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trav_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return false;
-    unsigned long long z[8] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trav_stats), z, sizeof(z));
-    return true;
-#else
-    (void)out;
-    return false;
-#endif
 }
 
 // NORI_SPLAT_SPLIT=0: one lane per pixel in the coded splat too.

@@ -889,6 +889,13 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     S.plane_c = scan_list.plane_c.empty() ? nullptr : c.plane_c.as<float>();
     S.plane_f = scan_list.plane_f.empty() ? nullptr : c.plane_f.as<float4>();
     for (int a = 0; a < 3; ++a) S.plane_end[a] = scan_list.plane_end[a];
+    {
+        const char *e = std::getenv("NORI_CAMERA_CULL");  // A/B and verification: 0 = no in-plane filter
+        S.camera_cull = !(e && e[0] == '0');
+        const char *t = std::getenv("NORI_TRACE_CULL");  // trace API: 0, 1 (default) or 2 (needs plane pairs)
+        S.trace_cull = t ? std::atoi(t) : 1;
+        if (S.trace_cull < 0 || S.trace_cull > 2 || (S.trace_cull == 2 && !S.plane_f)) S.trace_cull = 1;
+    }
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     S.blob = use_blob ? c.blob.as<float4>() : nullptr;
     S.blob_bytes = use_blob ? (uint32_t)blob.size() : 0u;
@@ -1013,7 +1020,6 @@ bool debug_log() {
 // 3089; C4 and C5 within 1 %).
 uint32_t pool_parts(bool bvh) {
     (void)bvh;
-    if (extend_mode() == 2) return 1u;  // NORI_EXTEND_CHECK: its scratch serves one stream
     const uint32_t def = 3u;
     const char *e = std::getenv("NORI_POOL_PARTS");
     const long v = e ? std::atol(e) : (long)def;
@@ -1463,30 +1469,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             finish_rays += st.w;
         }
         invalid += hc.invalid;
-        if (c.stack == 0 && extend_mode() == 2) {  // NORI_EXTEND_CHECK: the two extension kernels must agree
-            unsigned long long ck[4] = {0, 0, 0, 0};
-            if (extend_check_take(ck) && (debug_log() || ck[0] || ck[2])) {
-                std::fprintf(stderr, "[nori] extension check: %llu of %llu hit records differ\n", ck[0], ck[1]);
-                std::fprintf(stderr, "[nori] shadow check: %llu of %llu occlusions differ\n", ck[2], ck[3]);
-            }
-            if (ck[0] || ck[2])
-                throw NoriException(NORI_ERR_INVALID, "trace check: k_trace_bin differs from the scan on " +
-                                                          std::to_string(ck[0]) + " of " + std::to_string(ck[1]) +
-                                                          " extension rays and " + std::to_string(ck[2]) + " of " +
-                                                          std::to_string(ck[3]) + " shadow rays");
-        }
         if (debug_log())
         {
-            unsigned long long ep[4];
-            if (ext_prof_take(ep) && ep[3])
-                std::fprintf(stderr, "[nori] k_extend_scan clocks per wave: loads + prologue %.0f, scan %.0f, stores %.0f (%llu waves)\n",
-                             (double)ep[0] / ep[3], (double)ep[1] / ep[3], (double)ep[2] / ep[3], ep[3]);
-            unsigned long long ts[8];
-            if (trav_stats_take(ts) && ts[3])
-                std::fprintf(stderr, "[nori] BVH walks: %llu rays, per ray %.2f inner nodes, %.2f leaves, %.2f primitives; "
-                             "longest walk %llu visits, %llu rays over 64 visits (%.1f visits each)\n",
-                             ts[3], (double)ts[0] / ts[3], (double)ts[1] / ts[3], (double)ts[2] / ts[3], ts[4], ts[5],
-                             ts[5] ? (double)ts[6] / ts[5] : 0.0);
             std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays\n", p0,
                          (unsigned long)iters, hc.finish_paths, hc.finish_max_rays);
             if (hc.prof[6])  // NORI_PROF_SHADE builds

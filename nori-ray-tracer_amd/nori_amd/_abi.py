@@ -1,4 +1,4 @@
-"""ctypes mirror of include/nori_gpu.h (ABI version 5, _abi.ABI_VERSION).
+"""ctypes mirror of include/nori_gpu.h (ABI version 6, _abi.ABI_VERSION).
 
 The structures below must match the C declarations field for field; the
 test suite checks their sizes against the library (tests/test_abi.py).
@@ -6,7 +6,7 @@ test suite checks their sizes against the library (tests/test_abi.py).
 import ctypes as C
 import os
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 NORI_OK = 0
 NORI_ERR_INVALID = -1
