@@ -406,6 +406,10 @@ def main():
                             for k in ("closest", "shadow", "finish")},
             "per_rank_ms_per_step": rank_ms,
             "comm_nranks_per_rank": comm_ranks,
+            # scan-mode scenes: the scan kernels specialised for the scene through hipRTC at context
+            # creation (csrc/rtc.hip), outside the timed region; cached per process and on disk
+            "scan_kernels": {"specialised": bool(last.get("scan_rtc")), "compile_ms": last.get("ms_scan_rtc"),
+                             "from_cache": bool(last.get("scan_rtc_cached"))},
             "wavefront_iterations": last["iterations"],
             "stream_parts": last.get("stream_parts", 1),
             "hip_runtime": hip_runtime(),

@@ -44,7 +44,9 @@
 #ifndef NORI_GPU_H
 #define NORI_GPU_H
 
+#ifndef __HIPCC_RTC__  /* (the library compiles its scan kernels at run time with hipRTC, which has size_t built in) */
 #include <stddef.h>
+#endif
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -307,6 +309,14 @@ typedef struct nori_scan_info {
 int nori_scene_scan_list(const nori_scene_desc *scene, nori_scan_info *info, float *records, float *plane_c,
                          float *plane_f);
 
+/* Compiles the scene's scan kernels specialised for its scan list (the
+ * hipRTC program nori_gpu_create loads for scan-mode scenes, rtc.hip) for the
+ * target `arch` (e.g. "gfx950"), without a device: *code_bytes = the code
+ * object's size (0 for a BVH scene), *ms = the compile time (or cache read).
+ * NORI_ERR_UNSUPPORTED when hipRTC is missing or the compile fails
+ * (nori_gpu_last_error holds the log). */
+int nori_scene_scan_rtc(const nori_scene_desc *scene, const char *arch, size_t *code_bytes, double *ms);
+
 /* ---- GPU context ----------------------------------------------------------- */
 typedef struct nori_gpu_ctx nori_gpu_ctx;
 
@@ -342,6 +352,11 @@ typedef struct nori_gpu_stats {
     double ms_total;              /* render wall time (host timer)              */
     /* with desc.timing: summed HIP-event time of each kernel, on the launch stream */
     double ms_extend, ms_shadow, ms_shade, ms_splat, ms_finish;
+    /* scan-mode scenes: 1 when the scan kernels run specialised for this scene
+       (hipRTC at nori_gpu_create), the time that compile (or cache read) took
+       then, and 1 when its code object came from the cache */
+    uint32_t scan_rtc, scan_rtc_cached;
+    double ms_scan_rtc;
 } nori_gpu_stats;
 
 typedef struct nori_gpu_hit {

@@ -21,7 +21,9 @@
 // Shadow queue: ray_o, ray_d, payload float4 (contribution.rgb, work).
 // Sample records: float4 per camera sample (L.rgb, 0).
 #pragma once
+#ifndef __HIPCC_RTC__  // (hipRTC: the runtime header is built in)
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 #include "device_math.h"

@@ -5,7 +5,9 @@
 // reference's x86-64 build; transcendentals come from the ROCm device library
 // and may differ from glibc by a few ulp.
 #pragma once
+#ifndef __HIPCC_RTC__  // (hipRTC: the runtime header is built in)
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 #include "../../include/nori_gpu.h"

@@ -2,6 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string>
+#include <vector>
+
 #include "dev_scene.h"
 
 namespace nori {
@@ -39,16 +42,42 @@ struct SplatDesc {
     float *var;               // per-pixel sample statistics W x H x 8 (sum L, sum L^2, n) or null
 };
 
+// Scene-specialised scan kernels (rtc.hip): a scan-mode scene's scan list
+// compiled in as literals through hipRTC at context creation.
+struct ScanRtcScene {
+    const float *rec;  // 12 floats per record
+    uint32_t nrec;
+    const float *plane_c, *plane_f;  // per pair: 1 and 8 floats
+    uint32_t pairs;
+    uint32_t plane_end[3];
+    uint32_t tris, real;
+};
+struct ScanRtc {
+    hipModule_t mod = nullptr;
+    hipFunction_t extend = nullptr, shadow = nullptr, trace[2] = {nullptr, nullptr};  // trace[any_hit]
+    double compile_ms = 0.0;  // hipRTC compile (or cache read) at context creation
+    bool cached = false;      // the code object came from the process or disk cache
+    size_t code_bytes = 0;
+};
+std::string rtc_const_scene(const ScanRtcScene &sc);
+// Compiles (or finds cached) the specialised code object for target `arch`.
+bool rtc_compile(const ScanRtcScene &sc, const std::string &arch, int trace_cull, std::vector<char> &code, double &ms,
+                 bool &cached, std::string &why);
+// ... and loads it on the current device; false (with why) leaves `out` empty.
+bool scan_rtc_build(const ScanRtcScene &sc, int device, int trace_cull, ScanRtc &out, std::string &why);
+void scan_rtc_release(ScanRtc &r);
+
 // stack = LDS stack depth (8, 16, 32 or 64) chosen from the BVH depth.
+// rtc: the scene's specialised scan kernels, used for stack 0 when present.
 hipError_t launch_trace(const DevScene &S, const float4 *rays, uint32_t n, int any_hit, float4 *hits, int stack,
-                        hipStream_t st);
+                        hipStream_t st, const ScanRtc *rtc = nullptr);
 hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,
                         const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                         uint32_t nseg, hipStream_t st);
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
-                         hipStream_t st);
+                         hipStream_t st, const ScanRtc *rtc = nullptr);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
-                         int stack, hipStream_t st);
+                         int stack, hipStream_t st, const ScanRtc *rtc = nullptr);
 // Marks the record of every queued path pending (w = kRecPending, the jitter
 // class bits cleared): k_splat skips it, the finisher splats it itself.
 // Zeroes the counters and segment state of a chunk, Counters::exhausted = empty.

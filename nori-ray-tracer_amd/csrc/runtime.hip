@@ -207,6 +207,7 @@ struct nori_gpu_ctx {
     hipStream_t parts[kMaxParts] = {};  // parts[0] unused (part 0 runs on `stream`)
     hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
+    ScanRtc rtc;         // scan-mode scenes: the scan kernels specialised for this scene (rtc.hip), or empty
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, plane_c, plane_f;
     DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
@@ -240,6 +241,7 @@ struct nori_gpu_ctx {
             if (joins[h]) (void)hipEventDestroy(joins[h]);
             if (parts[h]) (void)hipStreamDestroy(parts[h]);
         }
+        scan_rtc_release(rtc);
         if (pinned) (void)hipHostFree(pinned);
         if (readback) (void)hipHostFree(readback);
         if (fork) (void)hipEventDestroy(fork);
@@ -896,6 +898,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         S.trace_cull = t ? std::atoi(t) : 1;
         if (S.trace_cull < 0 || S.trace_cull > 2 || (S.trace_cull == 2 && !S.plane_f)) S.trace_cull = 1;
     }
+    if (scan && scan_list.prims.size() / 12 <= 2 * kScanMaxPrims) {  // the scan kernels compiled for this scene's scan list (rtc.hip); else the generic ones
+        ScanRtcScene sc{scan_list.prims.data(), (uint32_t)(scan_list.prims.size() / 12), scan_list.plane_c.data(),
+                        scan_list.plane_f.data(), (uint32_t)scan_list.plane_c.size(),
+                        {scan_list.plane_end[0], scan_list.plane_end[1], scan_list.plane_end[2]}, scan_list.tris,
+                        scan_list.real};
+        std::string why;
+        if (!scan_rtc_build(sc, c.device, S.trace_cull, c.rtc, why) && debug_log())
+            std::fprintf(stderr, "[nori] generic scan kernels: %s\n", why.c_str());
+    }
     for (int k = 0; k < 3; ++k) S.root_min[k] = rmin[k], S.root_max[k] = rmax[k];
     S.blob = use_blob ? c.blob.as<float4>() : nullptr;
     S.blob_bytes = use_blob ? (uint32_t)blob.size() : 0u;
@@ -1398,9 +1409,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                     return launch_shade(S, Qh[h][in], Qh[h][out], sqh[h], sg, in, wdh[h], c.rec.as<float4>(), C,
                                         Gp[h], st);
                 });
-                timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st); });
+                timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st, &c.rtc); });
                 timed_on(st, 1, [&] {
-                    return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st);
+                    return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st, &c.rtc);
                 });
             }
             ++iters;
@@ -1535,6 +1546,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         stats->ms_splat = kms[3];
         stats->ms_finish = kms[4];
         stats->rays_finish = finish_rays;
+        stats->scan_rtc = c.rtc.extend ? 1u : 0u;
+        stats->scan_rtc_cached = c.rtc.cached ? 1u : 0u;
+        stats->ms_scan_rtc = c.rtc.compile_ms;
     }
     if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
     return NORI_OK;
@@ -1712,6 +1726,29 @@ int nori_scene_bvh_info(const nori_scene_desc *d, nori_bvh_info *out) {
         return NORI_OK;
     });
 }
+int nori_scene_scan_rtc(const nori_scene_desc *d, const char *arch, size_t *code_bytes, double *ms) {
+    return guarded([&] {
+        if (!d || !arch || !code_bytes || !ms) return fail(NORI_ERR_INVALID, "null argument");
+        if (d->abi_version != NORI_GPU_ABI_VERSION) return fail(NORI_ERR_INVALID, "ABI version mismatch");
+        float rmin[3], rmax[3];
+        scene_root_box(*d, rmin, rmax);
+        DeviceBvh bvh;
+        build_device_bvh(*d, rmin, rmax, bvh);
+        const uint32_t n = (uint32_t)(bvh.prims.size() / 12);
+        *code_bytes = 0;
+        *ms = 0.0;
+        if (n > kScanMaxPrims) return NORI_OK;  // a BVH scene: nothing to specialise
+        const ScanList L = build_scan_list(bvh, n);
+        ScanRtcScene sc{L.prims.data(), (uint32_t)(L.prims.size() / 12), L.plane_c.data(), L.plane_f.data(),
+                        (uint32_t)L.plane_c.size(), {L.plane_end[0], L.plane_end[1], L.plane_end[2]}, L.tris, L.real};
+        std::vector<char> code;
+        bool cached = false;
+        std::string why;
+        if (!rtc_compile(sc, arch, 1, code, *ms, cached, why)) return fail(NORI_ERR_UNSUPPORTED, why);
+        *code_bytes = code.size();
+        return NORI_OK;
+    });
+}
 int nori_scene_scan_list(const nori_scene_desc *d, nori_scan_info *info, float *records, float *plane_c,
                          float *plane_f) {
     return guarded([&] {
@@ -1808,7 +1845,7 @@ int nori_gpu_trace(nori_gpu_ctx *c, const float *rays, uint32_t n, int any_hit, 
         r.ensure(32 * (size_t)n);
         h.ensure(16 * (size_t)n);
         HIP_TRY(hipMemcpy(r.p, rays, 32 * (size_t)n, hipMemcpyHostToDevice));
-        HIP_TRY(launch_trace(c->S, r.as<float4>(), n, any_hit, h.as<float4>(), c->stack, c->stream));
+        HIP_TRY(launch_trace(c->S, r.as<float4>(), n, any_hit, h.as<float4>(), c->stack, c->stream, &c->rtc));
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(hipMemcpy(hits, h.p, 16 * (size_t)n, hipMemcpyDeviceToHost));
         return NORI_OK;

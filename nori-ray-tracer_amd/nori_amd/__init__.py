@@ -224,6 +224,15 @@ def scan_list(scene):
             "plane_end": np.array(list(info.plane_end)), "tris": info.tris}
 
 
+def scan_rtc(scene, arch="gfx950"):
+    """Compile the scene's scan kernels specialised for its scan list for `arch` (the hipRTC program
+    GpuRenderer loads for scan-mode scenes; no device needed): (code object bytes, milliseconds);
+    (0, 0.0) for a BVH scene."""
+    n, ms = C.c_size_t(), C.c_double()
+    check(lib().nori_scene_scan_rtc(scene.desc_ptr, arch.encode(), C.byref(n), C.byref(ms)))
+    return n.value, ms.value
+
+
 def read_exr(path):
     """R, G, B planes of an OpenEXR file as a (height, width, 3) float32 array (nori_read_exr)."""
     w, h = C.c_int(), C.c_int()

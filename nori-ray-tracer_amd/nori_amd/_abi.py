@@ -104,7 +104,8 @@ class Stats(C.Structure):
                 ("bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32), ("stream_parts", C.c_uint32),
                 ("path_pool", C.c_uint32), ("ms_total", C.c_double),
                 ("ms_extend", C.c_double), ("ms_shadow", C.c_double), ("ms_shade", C.c_double),
-                ("ms_splat", C.c_double), ("ms_finish", C.c_double)]
+                ("ms_splat", C.c_double), ("ms_finish", C.c_double),
+                ("scan_rtc", C.c_uint32), ("scan_rtc_cached", C.c_uint32), ("ms_scan_rtc", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -134,6 +135,7 @@ SIGNATURES = {
     "nori_scene_bvh_info": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nori_scene_scan_list": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float)]),
+    "nori_scene_scan_rtc": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_size_t), C.POINTER(C.c_double)]),
     "nori_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nori_gpu_create": (C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "nori_gpu_render": (C.c_int, [C.c_void_p, C.POINTER(RenderDesc), C.c_void_p, C.POINTER(Stats)]),
