@@ -55,6 +55,7 @@ struct ScanRtcScene {
 struct ScanRtc {
     hipModule_t mod = nullptr;
     hipFunction_t extend = nullptr, shadow = nullptr, trace[2] = {nullptr, nullptr};  // trace[any_hit]
+    int k_extend = 0;         // rays per thread of `extend`
     double compile_ms = 0.0;  // hipRTC compile (or cache read) at context creation
     bool cached = false;      // the code object came from the process or disk cache
     size_t code_bytes = 0;
@@ -66,6 +67,7 @@ bool rtc_compile(const ScanRtcScene &sc, const std::string &arch, int trace_cull
 // ... and loads it on the current device; false (with why) leaves `out` empty.
 bool scan_rtc_build(const ScanRtcScene &sc, int device, int trace_cull, ScanRtc &out, std::string &why);
 void scan_rtc_release(ScanRtc &r);
+int rtc_rays_per_thread();
 
 // stack = LDS stack depth (8, 16, 32 or 64) chosen from the BVH depth.
 // rtc: the scene's specialised scan kernels, used for stack 0 when present.

@@ -2242,7 +2242,8 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
         const dim3 gk(seg_grid(G, scan_per<kScanRays, NORI_EXTEND_BLOCK>())), bk(NORI_EXTEND_BLOCK);
         if (rtc && rtc->extend) {
             void *args[] = {(void *)&S, (void *)&q, (void *)&cnt, (void *)&G};
-            return hipModuleLaunchKernel(rtc->extend, gk.x, 1, 1, bk.x, 1, 1, 0, st, args, nullptr);
+            const uint32_t per = kTraceGroup * kSeg / (NORI_EXTEND_BLOCK * (uint32_t)rtc->k_extend);
+            return hipModuleLaunchKernel(rtc->extend, seg_grid(G, per), 1, 1, bk.x, 1, 1, 0, st, args, nullptr);
         }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
         return hipGetLastError();
