@@ -223,168 +223,6 @@ ND bool traverse(const DevScene &S, TRay r, uint32_t *stk, float &tb, uint32_t &
     return found;
 }
 
-// Two interleaved walks per lane (NORI_BVH_WALKS=2; the BVH scenes' trace
-// kernels, C3).  A walk is latency-bound: each node step waits for its
-// 128-byte node before it can choose the next.  A lane carrying two rays
-// alternates their steps -- process walk A's fetched item and issue the
-// fetch of its next one, then the same for walk B -- so that one walk's
-// fetch is in flight while the other's item is tested (s_waitcnt counts in
-// order: waiting for B's data leaves A's newer loads outstanding).  Each
-// walk is traverse<STACK, ANY> step for step (the same box tests, child
-// order, stack keys and leaf order), so the hits are the same.
-struct Walk {
-    TRay r;
-    float4 nd[7];      // the fetched item: an inner node (7 vectors) or a primitive record (3)
-    uint32_t ref;      // the item's reference: an inner node, or a leaf (bit 31) whose primitive i is fetched
-    uint32_t i, end;   // leaf: the fetched primitive and the leaf's end
-    int sp;
-    bool on, found;
-    float tb, ub, vb;
-    uint32_t pb;
-};
-ND void walk_fetch(const DevScene &S, Walk &w) {  // issue the loads of w.ref's item
-    if (!(w.ref & 0x80000000u)) {
-        load_node(S, w.ref, w.nd[0], w.nd[1], w.nd[2], w.nd[3], w.nd[4], w.nd[5], w.nd[6]);
-    } else {
-        w.i = w.ref & 0x1FFFFFFu;
-        w.end = w.i + ((w.ref >> 25) & 63u) + 1u;
-        const float4 *p = S.prims + 3 * (size_t)w.i;
-        w.nd[0] = gld(p), w.nd[1] = gld(p + 1), w.nd[2] = gld(p + 2);
-    }
-}
-template <int STACK>
-ND void walk_init(const DevScene &S, Walk &w, bool live) {
-    TRay &r = w.r;
-    if (r.mint == kEps) r.mint = smax(r.mint, r.mint * smax(smax(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z)));
-    w.tb = INF_F;
-    w.pb = 0xFFFFFFFFu;
-    w.ub = w.vb = 0.0f;
-    w.found = false;
-    w.sp = 0;
-    r.rcp = V3{rcp_full(r.d.x), rcp_full(r.d.y), rcp_full(r.d.z)};
-    w.on = live && !(r.maxt < r.mint);
-    w.ref = 0u;
-    if (w.on) walk_fetch(S, w);
-}
-// One step of walk w: test its fetched item, choose the next one and issue its fetch.
-template <int STACK, bool ANY>
-ND void walk_step(const DevScene &S, Walk &w, uint32_t *stk, uint32_t *spill, float *spillk) {
-    if (!w.on) return;
-    constexpr int L = stack_lds_entries(STACK);
-    bool pop = false;
-    if (!(w.ref & 0x80000000u)) {
-        const float4 mnx = w.nd[0], mny = w.nd[1], mnz = w.nd[2], mxx = w.nd[3], mxy = w.nd[4], mxz = w.nd[5],
-                     rf = w.nd[6];
-        float k0, k1, k2, k3;
-        const bool h0 = box_test(make_float4(mnx.x, mny.x, mnz.x, 0), make_float4(mxx.x, mxy.x, mxz.x, 0), w.r, k0);
-        const bool h1 = box_test(make_float4(mnx.y, mny.y, mnz.y, 0), make_float4(mxx.y, mxy.y, mxz.y, 0), w.r, k1);
-        const bool h2 = box_test(make_float4(mnx.z, mny.z, mnz.z, 0), make_float4(mxx.z, mxy.z, mxz.z, 0), w.r, k2);
-        const bool h3 = box_test(make_float4(mnx.w, mny.w, mnz.w, 0), make_float4(mxx.w, mxy.w, mxz.w, 0), w.r, k3);
-        k0 = h0 ? k0 : INF_F;
-        k1 = h1 ? k1 : INF_F;
-        k2 = h2 ? k2 : INF_F;
-        k3 = h3 ? k3 : INF_F;
-        const int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
-        if (nh > 0) {
-            uint32_t c0 = __float_as_uint(rf.x), c1 = __float_as_uint(rf.y), c2 = __float_as_uint(rf.z),
-                     c3 = __float_as_uint(rf.w);
-            bool m0 = !h0, m1 = !h1, m2 = !h2, m3 = !h3;
-            auto cs = [](float &ka, uint32_t &ca, bool &ma, float &kb, uint32_t &cb, bool &mb) {
-                const bool sw = ma > mb || (ma == mb && kb < ka);
-                const float tk = ka;
-                const uint32_t tc = ca;
-                const bool tm = ma;
-                ka = sw ? kb : ka;
-                kb = sw ? tk : kb;
-                ca = sw ? cb : ca;
-                cb = sw ? tc : cb;
-                ma = sw ? mb : ma;
-                mb = sw ? tm : mb;
-            };
-            cs(k0, c0, m0, k1, c1, m1);
-            cs(k2, c2, m2, k3, c3, m3);
-            cs(k0, c0, m0, k2, c2, m2);
-            cs(k1, c1, m1, k3, c3, m3);
-            cs(k1, c1, m1, k2, c2, m2);
-            auto push = [&](uint32_t v, float k) {
-                if (w.sp < L) {
-                    stk[w.sp * kTraceBlock] = v;
-                    if (NORI_STACK_KEYS) stk[(L + w.sp) * kTraceBlock] = __float_as_uint(k);
-                } else {
-                    spill[w.sp - L] = v;
-                    if (NORI_STACK_KEYS) spillk[w.sp - L] = k;
-                }
-                ++w.sp;
-            };
-            if (nh > 3) push(c3, k3);
-            if (nh > 2) push(c2, k2);
-            if (nh > 1) push(c1, k1);
-            w.ref = c0;
-        } else {
-            pop = true;
-        }
-    } else {
-        float t = 0, u = 0, v = 0;
-        bool h;
-        if (__float_as_uint(w.nd[1].w) == 0u) {
-            h = tri_hit(w.nd[0], w.nd[1], w.nd[2], w.r, t, u, v);
-        } else {
-            h = sphere_hit(w.nd[0], w.nd[1], w.r, t);
-            u = v = 0.0f;
-        }
-        if (h) {
-            w.found = true;
-            if (ANY) {
-                w.on = false;
-                return;
-            }
-            w.r.maxt = w.tb = t;
-            w.ub = u;
-            w.vb = v;
-            w.pb = __float_as_uint(w.nd[0].w);
-        }
-        if (++w.i < w.end) {  // the leaf's next primitive (leaf order, bvh.cpp:440-452)
-            const float4 *p = S.prims + 3 * (size_t)w.i;
-            w.nd[0] = gld(p), w.nd[1] = gld(p + 1), w.nd[2] = gld(p + 2);
-            return;
-        }
-        pop = true;
-    }
-    if (pop) {
-        bool next = false;
-        while (w.sp > 0) {
-            --w.sp;
-            w.ref = w.sp < L ? stk[w.sp * kTraceBlock] : spill[w.sp - L];
-            if (!NORI_STACK_KEYS) {
-                next = true;
-                break;
-            }
-            const float key = w.sp < L ? __uint_as_float(stk[(L + w.sp) * kTraceBlock]) : spillk[w.sp - L];
-            if (!(key > w.r.maxt)) {
-                next = true;
-                break;
-            }
-        }
-        if (!next) {
-            w.on = false;
-            return;
-        }
-    }
-    walk_fetch(S, w);
-}
-// Two walks (stk0, stk1: the lane's two LDS stack columns).
-template <int STACK, bool ANY>
-ND void traverse2(const DevScene &S, Walk (&w)[2], bool live0, bool live1, uint32_t *stk0, uint32_t *stk1) {
-    uint32_t spill[2][kTraceSpill];
-    float spillk[2][kTraceSpill];
-    walk_init<STACK>(S, w[0], live0);
-    walk_init<STACK>(S, w[1], live1);
-    while (w[0].on || w[1].on) {
-        walk_step<STACK, ANY>(S, w[0], stk0, spill[0], spillk[0]);
-        walk_step<STACK, ANY>(S, w[1], stk1, spill[1], spillk[1]);
-    }
-}
-
 template <int STACK, bool ANY>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene S, const float4 *rays, uint32_t n, float4 *hits) {
     if constexpr (STACK == 0) {  // the caller's rays: mint may be <= 0 (scan_core ZMINT)
@@ -449,46 +287,6 @@ ND void shadow_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *sh
     }
 }
 
-// The two-walk forms of extend_body / shadow_body: thread t of work-group j
-// of a group takes entries 2 j kTraceBlock + t and + kTraceBlock.
-constexpr uint32_t kTraceSlices2 = kTraceSlices / 2;
-template <int STACK>
-ND void extend2_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt, uint32_t G, uint32_t bid,
-                     uint32_t *stk) {
-    const SegRange sr = seg_group(cnt, G, bid, kTraceSlices2);
-    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(bid, kTraceSlices2, kTraceBlock, 2, threadIdx.x);
-    if (i0 >= n) return;
-    const uint32_t i1 = i0 + kTraceBlock;
-    const uint32_t q0 = seg_entry(sr, i0), q1 = seg_entry(sr, i1 < n ? i1 : i0);
-    Walk w[2];
-    path_ray(S, pq.ray_o[q0], pq.ray_d[q0], w[0].r);
-    path_ray(S, pq.ray_o[q1], pq.ray_d[q1], w[1].r);
-    traverse2<STACK, false>(S, w, true, i1 < n, stk + threadIdx.x, stk + stack_words(STACK) * kTraceBlock + threadIdx.x);
-    pq.hit[q0] = make_float4(w[0].tb, __uint_as_float(w[0].pb), w[0].ub, w[0].vb);
-    if (i1 < n) pq.hit[q1] = make_float4(w[1].tb, __uint_as_float(w[1].pb), w[1].ub, w[1].vb);
-}
-template <int STACK>
-ND void shadow2_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
-                     uint32_t bid, uint32_t *stk) {
-    const SegRange sr = seg_group(shcnt, G, bid, kTraceSlices2);
-    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(bid, kTraceSlices2, kTraceBlock, 2, threadIdx.x);
-    if (i0 >= n) return;
-    const uint32_t i1 = i0 + kTraceBlock;
-    const uint32_t q[2] = {seg_entry(sr, i0), seg_entry(sr, i1 < n ? i1 : i0)};
-    Walk w[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const float4 a = sq.ray_o[q[k]], b = sq.ray_d[q[k]];
-        w[k].r.o = ld3(a);
-        w[k].r.d = ld3(b);
-        w[k].r.mint = a.w;
-        w[k].r.maxt = b.w;
-    }
-    traverse2<STACK, true>(S, w, true, i1 < n, stk + threadIdx.x, stk + stack_words(STACK) * kTraceBlock + threadIdx.x);
-    if (!w[0].found) shadow_add(rec, sq.payload[q[0]]);
-    if (i1 < n && !w[1].found) shadow_add(rec, sq.payload[q[1]]);
-}
-
 #ifdef NORI_TRACE_WAVES
 #define NORI_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(NORI_TRACE_WAVES)))
 #else
@@ -518,17 +316,6 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
                                                         float4 *rec, uint32_t G) {
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
-}
-template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_extend2(DevScene S, PathQueue pq, const uint32_t *cnt, uint32_t G) {
-    __shared__ uint32_t stk[2 * stack_words(STACK) * kTraceBlock];
-    extend2_body<STACK>(S, pq, cnt, G, xcd_block(blockIdx.x, gridDim.x), stk);
-}
-template <int STACK>
-__global__ __launch_bounds__(kTraceBlock) void k_shadow2(DevScene S, ShadowQueue sq, const uint32_t *shcnt, float4 *rec,
-                                                         uint32_t G) {
-    __shared__ uint32_t stk[2 * stack_words(STACK) * kTraceBlock];
-    shadow2_body<STACK>(S, sq, shcnt, rec, G, xcd_block(blockIdx.x, gridDim.x), stk);
 }
 template <int K>
 __global__ __launch_bounds__(NORI_EXTEND_BLOCK) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
@@ -2528,14 +2315,6 @@ hipError_t launch_shade(const DevScene &S, const PathQueue &in, const PathQueue 
 
 #endif
 #if NORI_TU == 0
-// NORI_BVH_WALKS=2: two interleaved walks per lane in the BVH trace kernels.
-static int bvh_walks() {
-    static const int w = [] {
-        const char *e = std::getenv("NORI_BVH_WALKS");
-        return e && e[0] == '2' ? 2 : 1;
-    }();
-    return w;
-}
 hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *cnt, uint32_t G, int stack,
                          hipStream_t st, const ScanRtc *rtc) {
     dim3 g(seg_grid(G, kTraceSlices)), b(kTraceBlock);
@@ -2547,15 +2326,6 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
             return hipModuleLaunchKernel(rtc->extend, seg_grid(G, per), 1, 1, bk.x, 1, 1, 0, st, args, nullptr);
         }
         hipLaunchKernelGGL(k_extend_scan<kScanRays>, gk, bk, 0, st, S, q, cnt, G);
-        return hipGetLastError();
-    }
-    if (bvh_walks() == 2) {
-        const dim3 g2(seg_grid(G, kTraceSlices2));
-        switch (stack) {
-        case 8: hipLaunchKernelGGL(k_extend2<8>, g2, b, 0, st, S, q, cnt, G); break;
-        case 16: hipLaunchKernelGGL(k_extend2<16>, g2, b, 0, st, S, q, cnt, G); break;
-        default: hipLaunchKernelGGL(k_extend2<32>, g2, b, 0, st, S, q, cnt, G); break;
-        }
         return hipGetLastError();
     }
     switch (stack) {
@@ -2577,15 +2347,6 @@ hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_
             return hipModuleLaunchKernel(rtc->shadow, gk.x, 1, 1, bk.x, 1, 1, 0, st, args, nullptr);
         }
         hipLaunchKernelGGL(k_shadow_scan<kScanRaysShadow>, gk, bk, 0, st, S, sq, shcnt, rec, G);
-        return hipGetLastError();
-    }
-    if (bvh_walks() == 2) {
-        const dim3 g2(seg_grid(G, kTraceSlices2));
-        switch (stack) {
-        case 8: hipLaunchKernelGGL(k_shadow2<8>, g2, b, 0, st, S, sq, shcnt, rec, G); break;
-        case 16: hipLaunchKernelGGL(k_shadow2<16>, g2, b, 0, st, S, sq, shcnt, rec, G); break;
-        default: hipLaunchKernelGGL(k_shadow2<32>, g2, b, 0, st, S, sq, shcnt, rec, G); break;
-        }
         return hipGetLastError();
     }
     switch (stack) {
