@@ -59,7 +59,7 @@ from nori_amd._abi import BLOCK_SIZE  # noqa: E402
 
 METRIC = "Msamples/sec on cbox_path_mis 512×512@512spp; per-pixel L2 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PROFILE_TAG = "r05"  # committed rocprofv3 evidence: profiles/pmc_<tag>[_<config>].json (tools/pmc_to_profile.py)
+PROFILE_TAG = "r06"  # committed rocprofv3 evidence: profiles/pmc_<tag>[_<config>].json (tools/pmc_to_profile.py)
 VALU_PEAK = 256 * 4 * 2.4e9 / 2 * 64  # lane-instr/s: 256 CUs x 4 SIMDs, a wave64 VALU op per 2 cycles
 
 
@@ -154,16 +154,23 @@ def parity_full(scene, film, W, H, spp):
                 f"step's film), identical WAVE streams", oracle_s=secs)
 
 
-def profiled(prefix, config="c2"):
-    """Per-launch rocprofv3 numbers of the kernel whose name starts with `prefix`, if committed for this config."""
-    name = f"pmc_{PROFILE_TAG}.json" if config == "c2" else f"pmc_{PROFILE_TAG}_{config}.json"
+# the kernels a row of the roofline stands for: the scan-mode scenes' trace
+# kernels run as the scene-specialised hipRTC kernels (csrc/rtc.hip)
+KERNEL_NAMES = {"k_extend": ("nori_rtc_extend_scan", "k_extend"), "k_shadow": ("nori_rtc_shadow_scan", "k_shadow"),
+                "k_shade": ("k_shade",)}
+
+
+def profiled(name, config="c2"):
+    """Per-launch rocprofv3 numbers of the kernel `name` stands for (KERNEL_NAMES), if committed for this config."""
+    fname = f"pmc_{PROFILE_TAG}.json" if config == "c2" else f"pmc_{PROFILE_TAG}_{config}.json"
     try:
-        d = json.load(open(os.path.join(ROOT, "profiles", name)))
+        d = json.load(open(os.path.join(ROOT, "profiles", fname)))
     except (OSError, ValueError):
         return None
-    for k, v in d.get("kernels", {}).items():
-        if k.startswith(prefix):
-            return dict(v, name=k, file=f"profiles/{name}", commit=d.get("commit"))
+    for prefix in KERNEL_NAMES.get(name, (name,)):
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(prefix) and "hbm_bytes_per_launch" in v:
+                return dict(v, name=k, file=f"profiles/{fname}", commit=d.get("commit"))
     return None
 
 
