@@ -53,7 +53,7 @@ ND float4 gld(const float4 *p) {
 
 // One 4-wide BVH node: the child boxes in SoA form (mnx.x = child 0's min.x,
 // ...) and the four child references (exact 128-byte nodes; quantized
-// 64-byte nodes measured 9-12 % slower on C3 and the table scene).
+// 64-byte nodes measured 9-12 % slower on C3 and the table scene, DESIGN_LOG.md).
 ND void load_node(const DevScene &S, uint32_t ref, float4 &mnx, float4 &mny, float4 &mnz, float4 &mxx, float4 &mxy,
                   float4 &mxz, float4 &rf) {
     const float4 *nd = S.nodes + 8 * (size_t)ref;
@@ -1022,7 +1022,7 @@ ND bool glass_bounce(const DevShape &sh, const DevBsdf &B, PathState &ps, float 
 // caller runs the bounce through glass_bounce / chord_hit, which produce the
 // refraction, the Russian-roulette end or the exit.  (sqrtf and the
 // divisions are the IEEE sequences: the range-checked fast forms' branches
-// measured slower here, DESIGN.md.)
+// measured slower here)
 template <int INTEG>
 ND bool glass_step(const DevShape &sh, const DevBsdf &B, PathState &ps, float &t) {
     const V3 c = V3{sh.center[0], sh.center[1], sh.center[2]};
@@ -2055,7 +2055,7 @@ hipError_t launch_photons(const DevScene &S, uint64_t e0, uint32_t n, uint32_t *
 // waves on a SIMD (3 x 112 + 144 <= 512).  Measured (C2): splat 1.14-1.18 ms
 // and finisher 1.15-1.17 ms against 1.26-1.33 / 1.10-1.15 ms for 512 threads
 // with 8 records; 768 threads with 8 records (136 VGPRs) splat in 0.83 ms
-// but starve the finisher (1.75 ms), DESIGN.md section 5.
+// but starve the finisher (1.75 ms), DESIGN_LOG.md (round 5).
 #ifndef NORI_SPLAT_SPLIT_BLOCK
 #define NORI_SPLAT_SPLIT_BLOCK 768
 #endif

@@ -803,7 +803,7 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     // traversal stack: at most 3 entries per level of the 4-wide tree; the
     // first `stack` live in LDS, up to kTraceSpill more in private memory
     // (an 8-wide tree, 256-B nodes with a 19-comparator child order, was
-    // measured 15 % slower on C3 in round 5: DESIGN.md section 5)
+    // measured 15 % slower on C3 in round 5: DESIGN_LOG.md)
     const uint32_t need = 3 * bvh.depth + 1;
     // (LDS budget 16 words: measured best on the 22.7k and 524k triangle
     // scenes -- occupancy beats a deeper LDS part; 32 only when the spill
