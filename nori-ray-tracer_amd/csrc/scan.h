@@ -518,9 +518,6 @@ ND void extend_scan_body(const DevScene &S, const PathQueue &pq, const uint32_t 
         if (i0 + k * STEP < n) pq.hit[q[k]] = make_float4(t[k], __uint_as_float(p[k]), u[k], v[k]);
 }
 
-#ifndef NORI_SHADOW_PREFETCH  // 1: read the sample records before the scan (hipRTC: NORI_RTC_SHADOW_PREFETCH)
-#define NORI_SHADOW_PREFETCH 0
-#endif
 // k_shadow_scan: any hit of the shadow queue's rays; an unoccluded ray adds
 // its payload to its sample record.
 template <int K>
@@ -549,25 +546,10 @@ ND void shadow_scan_body(const DevScene &S, const ShadowQueue &sq, const uint32_
     float t[K], u[K], v[K];
     uint32_t p[K];
     bool f[K];
-#if NORI_SHADOW_PREFETCH
-    // the records read before the scan (every valid ray, occluded or not), so
-    // that their latency hides behind the tests; the same sums as shadow_add
-    // (the record belongs to this ray's path alone during the launch)
-    float4 Lr[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        if (valid[k]) Lr[k] = rec[__float_as_uint(c[k].w)];
-    scan_rays<K, true>(S, r, live, t, p, u, v, f);
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        if (valid[k] && !f[k])
-            rec[__float_as_uint(c[k].w)] = make_float4(Lr[k].x + c[k].x, Lr[k].y + c[k].y, Lr[k].z + c[k].z, Lr[k].w);
-#else
     scan_rays<K, true>(S, r, live, t, p, u, v, f);
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (valid[k] && !f[k]) shadow_add(rec, c[k]);
-#endif
 }
 
 
