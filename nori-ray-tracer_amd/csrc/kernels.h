@@ -55,6 +55,7 @@ struct ScanRtcScene {
 struct ScanRtc {
     hipModule_t mod = nullptr;
     hipFunction_t extend = nullptr, shadow = nullptr, trace[2] = {nullptr, nullptr};  // trace[any_hit]
+    hipFunction_t both = nullptr;  // extension + shadow rays of one iteration in one launch (launch_trace_both)
     int k_extend = 0;         // rays per thread of `extend`
     double compile_ms = 0.0;  // hipRTC compile (or cache read) at context creation
     bool cached = false;      // the code object came from the process or disk cache
@@ -80,6 +81,11 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
                          hipStream_t st, const ScanRtc *rtc = nullptr);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st, const ScanRtc *rtc = nullptr);
+// Both trace launches of an iteration as one (the specialised scan kernels
+// only); false: nothing launched, use launch_extend + launch_shadow.
+bool launch_trace_both(const DevScene &S, const PathQueue &q, const uint32_t *cnt, const ShadowQueue &sq,
+                       const uint32_t *shcnt, float4 *rec, uint32_t G, const ScanRtc *rtc, hipStream_t st,
+                       hipError_t &err);
 // Marks the record of every queued path pending (w = kRecPending, the jitter
 // class bits cleared): k_splat skips it, the finisher splats it itself.
 // Zeroes the counters and segment state of a chunk, Counters::exhausted = empty.

@@ -320,12 +320,12 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
 template <int K>
 __global__ __launch_bounds__(NORI_EXTEND_BLOCK) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
                                                                    uint32_t G) {
-    extend_scan_body<K>(S, pq, cnt, G);
+    extend_scan_body<K>(S, pq, cnt, G, blockIdx.x);
 }
 template <int K>
 __global__ __launch_bounds__(NORI_SHADOW_BLOCK) void k_shadow_scan(DevScene S, ShadowQueue sq, const uint32_t *shcnt,
                                                                    float4 *rec, uint32_t G) {
-    shadow_scan_body<K>(S, sq, shcnt, rec, G);
+    shadow_scan_body<K>(S, sq, shcnt, rec, G, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ shading helpers
@@ -2337,6 +2337,17 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
     return hipGetLastError();
 }
 
+bool launch_trace_both(const DevScene &S, const PathQueue &q, const uint32_t *cnt, const ShadowQueue &sq,
+                       const uint32_t *shcnt, float4 *rec, uint32_t G, const ScanRtc *rtc, hipStream_t st,
+                       hipError_t &err) {
+    static_assert(NORI_EXTEND_BLOCK == NORI_SHADOW_BLOCK, "one work-group size for both roles");
+    if (!rtc || !rtc->both) return false;
+    uint32_t nb_ext = seg_grid(G, kTraceGroup * kSeg / (NORI_EXTEND_BLOCK * (uint32_t)rtc->k_extend));
+    const uint32_t nb = nb_ext + seg_grid(G, scan_per<kScanRaysShadow, NORI_SHADOW_BLOCK>());
+    void *args[] = {(void *)&S, (void *)&q, (void *)&cnt, (void *)&sq, (void *)&shcnt, (void *)&rec, (void *)&G, (void *)&nb_ext};
+    err = hipModuleLaunchKernel(rtc->both, nb, 1, 1, NORI_EXTEND_BLOCK, 1, 1, 0, st, args, nullptr);
+    return true;
+}
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st, const ScanRtc *rtc) {
     dim3 g(seg_grid(G, kTraceSlices)), b(kTraceBlock);

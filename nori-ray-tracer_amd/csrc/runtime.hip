@@ -1399,7 +1399,22 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipEventRecord(c.fork, c.stream));  // the part streams start after the resets above
         for (uint32_t h = 1; h < parts; ++h) HIP_TRY(hipStreamWaitEvent(c.parts[h], c.fork, 0));
         uint64_t lag = kLookahead;
+        // the specialised scan kernels' extension and shadow launches of a part
+        // as one (launch_trace_both; NORI_TRACE_FUSE=0: two launches)
+        const bool fuse_trace = [] {
+            const char *e = std::getenv("NORI_TRACE_FUSE");
+            return !(e && e[0] == '0');
+        }();
+        // NORI_DEBUG: host time spent enqueuing vs waiting on the ring events
+        // (a wait that returns at once means the device ran dry of work)
+        const bool dbg = debug_log();
+        double t_enq = 0.0, t_wait = 0.0;
+        uint32_t idle_waits = 0;
+        auto now_us = [] {
+            return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        };
         for (uint64_t it = 0;; ++it) {
+            const double te0 = dbg ? now_us() : 0.0;
             int in = (int)(it & 1), out = in ^ 1;
             last_out = out;
             for (uint32_t h = 0; h < parts; ++h) {
@@ -1409,6 +1424,13 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                     return launch_shade(S, Qh[h][in], Qh[h][out], sqh[h], sg, in, wdh[h], c.rec.as<float4>(), C,
                                         Gp[h], st);
                 });
+                hipError_t both_err = hipSuccess;
+                if (!timing && fuse_trace &&
+                    launch_trace_both(S, Qh[h][out], sg.cnt[out], sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], &c.rtc,
+                                      st, both_err)) {
+                    HIP_TRY(both_err);  // (the timed renders keep two launches: one event span per kernel)
+                    continue;
+                }
                 timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st, &c.rtc); });
                 timed_on(st, 1, [&] {
                     return launch_shadow(S, sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack, st, &c.rtc);
@@ -1420,8 +1442,15 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             const uint64_t ev = it;
             for (uint32_t h = 0; h < parts; ++h)
                 HIP_TRY(hipEventRecord(c.ring[h][ev % kRing], h ? c.parts[h] : c.stream));
+            const double te1 = dbg ? now_us() : 0.0;
+            t_enq += te1 - te0;
             if (ev >= lag) {
                 for (uint32_t h = 0; h < parts; ++h) HIP_TRY(hipEventSynchronize(c.ring[h][(ev - lag) % kRing]));
+                if (dbg) {
+                    const double w = now_us() - te1;
+                    t_wait += w;
+                    idle_waits += w < 5.0 ? 1u : 0u;
+                }
                 uint32_t exhausted = __atomic_load_n(&c.pinned[1], __ATOMIC_ACQUIRE);
                 // the streams are running dry: queue fewer iterations ahead,
                 // so that few drain iterations (full-grid launches over a
@@ -1484,6 +1513,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         {
             std::fprintf(stderr, "[nori] chunk %u: %lu iterations, finisher %u paths, longest %u rays\n", p0,
                          (unsigned long)iters, hc.finish_paths, hc.finish_max_rays);
+            std::fprintf(stderr, "[nori] host loop: %.0f us enqueuing, %.0f us waiting; %u of the waits returned at once\n",
+                         t_enq, t_wait, idle_waits);
             if (hc.prof[6])  // NORI_PROF_SHADE builds
                 std::fprintf(stderr, "[nori] shade clocks per wave: loads %.0f shade %.0f compact %.0f store %.0f regen %.0f drain %.0f (%llu waves)\n",
                              (double)hc.prof[0] / hc.prof[6], (double)hc.prof[1] / hc.prof[6],

@@ -481,12 +481,12 @@ constexpr uint32_t scan_per() {  // work-groups per group of kTraceGroup segment
 }
 // k_extend_scan: the closest hits of the path queue's extension rays.
 template <int K>
-ND void extend_scan_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt, uint32_t G) {
-    const SegRange sr = seg_group(cnt, G, blockIdx.x, scan_per<K, NORI_EXTEND_BLOCK>());
+ND void extend_scan_body(const DevScene &S, const PathQueue &pq, const uint32_t *cnt, uint32_t G, uint32_t bid) {
+    const SegRange sr = seg_group(cnt, G, bid, scan_per<K, NORI_EXTEND_BLOCK>());
     // a lane's K rays are entries NORI_EXTEND_BLOCK apart (adjacent entries, so
     // that a wave covers 64 K consecutive ones, measured 1 % slower)
     constexpr uint32_t STEP = NORI_EXTEND_BLOCK;
-    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(blockIdx.x, scan_per<K, NORI_EXTEND_BLOCK>(), NORI_EXTEND_BLOCK, K, threadIdx.x);
+    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(bid, scan_per<K, NORI_EXTEND_BLOCK>(), NORI_EXTEND_BLOCK, K, threadIdx.x);
     if (i0 >= n) return;  // entries fill the slice from its start
     TRay r[K];
     bool live[K];
@@ -521,9 +521,10 @@ ND void extend_scan_body(const DevScene &S, const PathQueue &pq, const uint32_t 
 // k_shadow_scan: any hit of the shadow queue's rays; an unoccluded ray adds
 // its payload to its sample record.
 template <int K>
-ND void shadow_scan_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G) {
-    const SegRange sr = seg_group(shcnt, G, blockIdx.x, scan_per<K, NORI_SHADOW_BLOCK>());
-    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(blockIdx.x, scan_per<K, NORI_SHADOW_BLOCK>(), NORI_SHADOW_BLOCK, K, threadIdx.x);
+ND void shadow_scan_body(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
+                         uint32_t bid) {
+    const SegRange sr = seg_group(shcnt, G, bid, scan_per<K, NORI_SHADOW_BLOCK>());
+    const uint32_t n = sr.pre[kTraceGroup], i0 = seg_first(bid, scan_per<K, NORI_SHADOW_BLOCK>(), NORI_SHADOW_BLOCK, K, threadIdx.x);
     if (i0 >= n) return;
     TRay r[K];
     bool live[K], valid[K];
