@@ -81,10 +81,11 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
                          hipStream_t st, const ScanRtc *rtc = nullptr);
 hipError_t launch_shadow(const DevScene &S, const ShadowQueue &sq, const uint32_t *shcnt, float4 *rec, uint32_t G,
                          int stack, hipStream_t st, const ScanRtc *rtc = nullptr);
-// Both trace launches of an iteration as one (the specialised scan kernels
-// only); false: nothing launched, use launch_extend + launch_shadow.
+// Both trace launches of an iteration as one (the BVH walks, or the
+// specialised scan kernels); false: nothing launched (a scan scene without
+// them), use launch_extend + launch_shadow.
 bool launch_trace_both(const DevScene &S, const PathQueue &q, const uint32_t *cnt, const ShadowQueue &sq,
-                       const uint32_t *shcnt, float4 *rec, uint32_t G, const ScanRtc *rtc, hipStream_t st,
+                       const uint32_t *shcnt, float4 *rec, uint32_t G, int stack, const ScanRtc *rtc, hipStream_t st,
                        hipError_t &err);
 // Marks the record of every queued path pending (w = kRecPending, the jitter
 // class bits cleared): k_splat skips it, the finisher splats it itself.

@@ -317,6 +317,18 @@ __global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_shadow(DevScene
     __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
     shadow_body<STACK>(S, sq, shcnt, rec, G, STACK ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x, stk);
 }
+// An iteration's extension and shadow walks in one launch (launch_trace_both):
+// work-groups [0, nb_ext) walk the extension rays, the rest the shadow rays
+// (independent queues); nb_ext is a multiple of the 8 XCDs, so both ranges
+// keep their XCD-aware order.
+template <int STACK>
+__global__ __launch_bounds__(kTraceBlock) NORI_TRACE_ATTR void k_trace_both(DevScene S, PathQueue pq, const uint32_t *cnt,
+                                                                            ShadowQueue sq, const uint32_t *shcnt,
+                                                                            float4 *rec, uint32_t G, uint32_t nb_ext) {
+    __shared__ uint32_t stk[stack_words(STACK) * kTraceBlock];
+    if (blockIdx.x < nb_ext) extend_body<STACK>(S, pq, cnt, G, xcd_block(blockIdx.x, nb_ext), stk);
+    else shadow_body<STACK>(S, sq, shcnt, rec, G, xcd_block(blockIdx.x - nb_ext, gridDim.x - nb_ext), stk);
+}
 template <int K>
 __global__ __launch_bounds__(NORI_EXTEND_BLOCK) void k_extend_scan(DevScene S, PathQueue pq, const uint32_t *cnt,
                                                                    uint32_t G) {
@@ -2338,9 +2350,21 @@ hipError_t launch_extend(const DevScene &S, const PathQueue &q, const uint32_t *
 }
 
 bool launch_trace_both(const DevScene &S, const PathQueue &q, const uint32_t *cnt, const ShadowQueue &sq,
-                       const uint32_t *shcnt, float4 *rec, uint32_t G, const ScanRtc *rtc, hipStream_t st,
+                       const uint32_t *shcnt, float4 *rec, uint32_t G, int stack, const ScanRtc *rtc, hipStream_t st,
                        hipError_t &err) {
     static_assert(NORI_EXTEND_BLOCK == NORI_SHADOW_BLOCK, "one work-group size for both roles");
+    if (stack != 0) {  // BVH walks
+        static_assert(kTraceSlices % kXcds == 0, "the shadow range starts on an XCD boundary");
+        const uint32_t nbe = seg_grid(G, kTraceSlices), nbt = 2 * nbe;
+        switch (stack) {
+        case 8: hipLaunchKernelGGL(k_trace_both<8>, dim3(nbt), dim3(kTraceBlock), 0, st, S, q, cnt, sq, shcnt, rec, G, nbe); break;
+        case 16: hipLaunchKernelGGL(k_trace_both<16>, dim3(nbt), dim3(kTraceBlock), 0, st, S, q, cnt, sq, shcnt, rec, G, nbe); break;
+        case 32: hipLaunchKernelGGL(k_trace_both<32>, dim3(nbt), dim3(kTraceBlock), 0, st, S, q, cnt, sq, shcnt, rec, G, nbe); break;
+        default: hipLaunchKernelGGL(k_trace_both<64>, dim3(nbt), dim3(kTraceBlock), 0, st, S, q, cnt, sq, shcnt, rec, G, nbe); break;
+        }
+        err = hipGetLastError();
+        return true;
+    }
     if (!rtc || !rtc->both) return false;
     uint32_t nb_ext = seg_grid(G, kTraceGroup * kSeg / (NORI_EXTEND_BLOCK * (uint32_t)rtc->k_extend));
     const uint32_t nb = nb_ext + seg_grid(G, scan_per<kScanRaysShadow, NORI_SHADOW_BLOCK>());

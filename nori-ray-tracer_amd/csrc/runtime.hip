@@ -1426,8 +1426,8 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                 });
                 hipError_t both_err = hipSuccess;
                 if (!timing && fuse_trace &&
-                    launch_trace_both(S, Qh[h][out], sg.cnt[out], sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], &c.rtc,
-                                      st, both_err)) {
+                    launch_trace_both(S, Qh[h][out], sg.cnt[out], sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack,
+                                      &c.rtc, st, both_err)) {
                     HIP_TRY(both_err);  // (the timed renders keep two launches: one event span per kernel)
                     continue;
                 }
