@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 cfgs=$1
 shift
 PT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 500 $PT tests/test_gpu_extend_bin.py tests/test_gpu_parity.py -k "not multirank" > gpurun_out/abcheck.log 2>&1
+timeout -k 10 500 $PT tests/test_gpu_pair_filter.py tests/test_gpu_parity.py -k "not multirank" > gpurun_out/abcheck.log 2>&1
 r=$?; echo "tests rc=$r: $(tail -1 gpurun_out/abcheck.log)"; [ $r -eq 0 ] || exit $r
 rm -f gpurun_out/ab_results.txt
 bash tools/gpu_ab.sh "$cfgs" "$@"

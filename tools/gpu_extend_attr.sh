@@ -1,11 +1,10 @@
 #!/bin/bash
 # Issue-slot attribution of the scan-mode extension kernel (k_extend_scan) on
 # the roofline render of bench.py (one pool part, kernels serialised): the
-# counters rocprofv3 can collect here, SQ counter passes of the default
-# library, then the wave phase clocks of the NORI_PROF_EXTEND build
-# (lib/libnori_gpu_prof.so: s_memtime stamps per wave -- ray loads + prologue,
-# scan, hit stores).  Every step has its own time limit; the script stops at
-# the first failure.
+# counters rocprofv3 can collect here and SQ counter passes of the default
+# library (the round-5 NORI_PROF_EXTEND stamp build is gone; a
+# lib/libnori_gpu_prof.so, if present, is run with NORI_DEBUG).  Every step
+# has its own time limit; the script stops at the first failure.
 # usage: tools/gpu_extend_attr.sh <tag> [bench args...]
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
