@@ -208,6 +208,9 @@ struct nori_gpu_ctx {
     hipEvent_t joins[kMaxParts] = {};
     DevScene S{};
     ScanRtc rtc;         // scan-mode scenes: the scan kernels specialised for this scene (rtc.hip), or empty
+    // an iteration's extension and shadow rays of a part in one launch
+    // (launch_trace_both); NORI_TRACE_FUSE=0 at creation: two launches
+    bool fuse_trace = true;
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, plane_c, plane_f;
     DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
@@ -1399,12 +1402,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         HIP_TRY(hipEventRecord(c.fork, c.stream));  // the part streams start after the resets above
         for (uint32_t h = 1; h < parts; ++h) HIP_TRY(hipStreamWaitEvent(c.parts[h], c.fork, 0));
         uint64_t lag = kLookahead;
-        // the specialised scan kernels' extension and shadow launches of a part
-        // as one (launch_trace_both; NORI_TRACE_FUSE=0: two launches)
-        const bool fuse_trace = [] {
-            const char *e = std::getenv("NORI_TRACE_FUSE");
-            return !(e && e[0] == '0');
-        }();
         // NORI_DEBUG: host time spent enqueuing vs waiting on the ring events
         // (a wait that returns at once means the device ran dry of work)
         const bool dbg = debug_log();
@@ -1425,7 +1422,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                                         Gp[h], st);
                 });
                 hipError_t both_err = hipSuccess;
-                if (!timing && fuse_trace &&
+                if (!timing && c.fuse_trace &&
                     launch_trace_both(S, Qh[h][out], sg.cnt[out], sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack,
                                       &c.rtc, st, both_err)) {
                     HIP_TRY(both_err);  // (the timed renders keep two launches: one event span per kernel)
@@ -1844,6 +1841,7 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         std::unique_ptr<nori_gpu_ctx> c(new nori_gpu_ctx);
         c->device = device;
         c->spp = d->sample_count ? d->sample_count : 1;
+        if (const char *e = std::getenv("NORI_TRACE_FUSE"); e && e[0] == '0') c->fuse_trace = false;
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         for (int h = 1; h < kMaxParts; ++h) {
