@@ -1500,8 +1500,10 @@ __global__ __launch_bounds__(1024) void k_tail_prefix(const uint32_t *cnt, uint3
 #ifndef NORI_FINISH_WAVES  // 0: 64 paths per wave
 // 2048 since the glass-sphere chain (round 3): fewer finisher waves leave the
 // film splat beside it more of the chip; 64-spp share 3446 -> 3550 (4096) ->
-// 3652 (2048) Msamples/s, 512 spp 4737 -> 4753 / 4744 (one box, interleaved)
-#define NORI_FINISH_WAVES 2048
+// 3652 (2048) Msamples/s, 512 spp 4737 -> 4753 / 4744 (one box, interleaved).
+// 1024 since round 6's shorter glass chain: 64-spp share 4677 -> 4725 (4
+// reps, every 1024 run above every 2048 run), 512 spp 5843 / 5834 (noise)
+#define NORI_FINISH_WAVES 1024
 #endif
 constexpr uint32_t kFinishWaves = NORI_FINISH_WAVES;
 #ifndef NORI_FINISH_GLASS  // 0: the tail finisher shades glass-sphere vertices generically
