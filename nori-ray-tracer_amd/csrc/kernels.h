@@ -92,8 +92,11 @@ bool launch_trace_both(const DevScene &S, const PathQueue &q, const uint32_t *cn
 // Zeroes the counters and segment state of a chunk, Counters::exhausted = empty.
 hipError_t launch_reset(Counters *C, uint32_t empty, const SegState &seg, uint32_t G, hipStream_t st);
 hipError_t launch_mark(const PathQueue &Q, const SegState &seg, int sel, float4 *rec, uint32_t G, hipStream_t st);
+// The prefix over the segments' path counts that numbers the tail's paths
+// (pre: G + 1 words); launch_finish reads it.
+hipError_t launch_tail_prefix(const SegState &seg, int sel, uint32_t G, uint32_t *pre, hipStream_t st);
 // Completes every queued path and splats its sample into `film` itself.
-// (pre: G + 1 words of scratch for the prefix over the segment counts)
+// (after launch_tail_prefix on the same stream)
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                          hipStream_t st);

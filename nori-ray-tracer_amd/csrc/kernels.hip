@@ -2426,7 +2426,6 @@ template <int INTEG, int VAR>
 static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                             const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,
                             hipStream_t st) {
-    hipLaunchKernelGGL(k_tail_prefix, dim3(1), dim3(1024), 0, st, seg.cnt[sel], G, pre);
     // enough waves for any path count n <= 256 G (kFinishWaves, or n / 64 <= 4 G when
     // K = 64); the idle blocks exit at once
     constexpr uint32_t wpb = kTraceBlock / 64;  // waves per block
@@ -2451,6 +2450,10 @@ static void finish_dispatch(const DevScene &S, const PathQueue &Q, const SegStat
     if (S.basic) finish_dispatch<INTEG, 0>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else if (S.chroma) finish_dispatch<INTEG, 2>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
     else finish_dispatch<INTEG, 1>(S, Q, seg, sel, rec, wd, film, C, G, stack, pre, st);
+}
+hipError_t launch_tail_prefix(const SegState &seg, int sel, uint32_t G, uint32_t *pre, hipStream_t st) {
+    hipLaunchKernelGGL(k_tail_prefix, dim3(1), dim3(1024), 0, st, seg.cnt[sel], G, pre);
+    return hipGetLastError();
 }
 hipError_t launch_finish(const DevScene &S, const PathQueue &Q, const SegState &seg, int sel, float4 *rec,
                          const WorkDesc &wd, float *film, Counters *C, uint32_t G, int stack, uint32_t *pre,

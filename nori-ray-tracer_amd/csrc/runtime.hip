@@ -211,6 +211,8 @@ struct nori_gpu_ctx {
     // an iteration's extension and shadow rays of a part in one launch
     // (launch_trace_both); NORI_TRACE_FUSE=0 at creation: two launches
     bool fuse_trace = true;
+    // the tail's finisher enqueued before the film splat beside it (NORI_FINISH_FIRST=0: after)
+    bool finish_first = true;
     nori_camera_desc cam{};
     DevBuf nodes, prims, tri_vidx, pos, nrm, prim_shape, shapes, bsdfs, emitters, cdf, env, blob, plane_c, plane_f;
     DevBuf tex;          // ImageTexture / NormalMap texels (RGBX8), global memory
@@ -1473,14 +1475,29 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         // pending ones and splats each itself.
         hipStream_t splat_st = c.side;
         HIP_TRY(launch_mark(Q[last_out], seg, last_out, c.rec.as<float4>(), G, c.stream));
+        HIP_TRY(launch_tail_prefix(seg, last_out, G, c.tailpre.as<uint32_t>(), c.stream));
         HIP_TRY(hipEventRecord(c.fork, c.stream));
         HIP_TRY(hipStreamWaitEvent(c.side, c.fork, 0));
         SplatDesc sd{M, np, rd.pass_begin + p0, std::max<uint32_t>(1, splat_passes(np, blocks.size())),
                      c.blocks.as<int4>(), rd.seed, var};
-        timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
-        timed(4, [&] {
-            return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack, c.tailpre.as<uint32_t>(), c.stream);
-        });
+        auto splat = [&] {
+            timed_on(splat_st, 3, [&] { return launch_splat(S, c.rec.as<float4>(), sd, (uint32_t)blocks.size(), film, C, splat_st); });
+        };
+        auto finish = [&] {
+            timed(4, [&] {
+                return launch_finish(S, Q[last_out], seg, last_out, c.rec.as<float4>(), wd, film, C, G, c.stack,
+                                     c.tailpre.as<uint32_t>(), c.stream);
+            });
+        };
+        // both wait for the same fork; the finisher's waves are enqueued first
+        // (c.finish_first) so that they are resident before the splat fills the CUs
+        if (c.finish_first) {
+            finish();
+            splat();
+        } else {
+            splat();
+            finish();
+        }
         HIP_TRY(hipEventRecord(c.join, c.side));
         HIP_TRY(hipStreamWaitEvent(c.stream, c.join, 0));
         // read-back through pinned staging: both copies queue behind the
@@ -1842,6 +1859,7 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         c->device = device;
         c->spp = d->sample_count ? d->sample_count : 1;
         if (const char *e = std::getenv("NORI_TRACE_FUSE"); e && e[0] == '0') c->fuse_trace = false;
+        if (const char *e = std::getenv("NORI_FINISH_FIRST"); e && e[0] == '0') c->finish_first = false;
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         for (int h = 1; h < kMaxParts; ++h) {
