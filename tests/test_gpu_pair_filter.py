@@ -159,3 +159,30 @@ def test_fused_trace_launch_same_image(built, parts, traversal):
     finally:
         fused.close()
         split.close()
+
+
+@pytest.mark.parametrize("parts", TRACE_SCENES, ids=["/".join(p[1:]) for p in TRACE_SCENES])
+def test_specialised_scan_same_hits(built, parts):
+    """The scan compiled for the scene through hipRTC (csrc/rtc.hip: the scan list as
+    literal operands) against the library's generic scan (NORI_RTC=0), on the same
+    adversarial rays, with each pair-skip mode: t, primitive and u bit for bit,
+    occlusion equal -- and the context reports which one it runs."""
+    s = nori_amd.load_scene(scene_path(*parts), 64, 48, 4)
+    rays = _ray_set(s, 37)
+    sh = rays.copy()
+    sh[:, 7] = np.random.default_rng(38).uniform(0.01, 2.0, size=sh.shape[0]).astype(f32)
+    for cull in ("0", "1", "2"):
+        spec, gen = _renderer(s, NORI_TRACE_CULL=cull), _renderer(s, NORI_TRACE_CULL=cull, NORI_RTC="0")
+        try:
+            a, b = spec.trace(rays), gen.trace(rays)
+            assert np.array_equal(a["t"].view(np.uint32), b["t"].view(np.uint32)), cull
+            assert np.array_equal(a["prim"], b["prim"]), cull
+            assert np.array_equal(a["u"].view(np.uint32), b["u"].view(np.uint32)), cull
+            assert np.array_equal(spec.trace(sh, any_hit=True)["prim"] >= 0, gen.trace(sh, any_hit=True)["prim"] >= 0)
+            if cull == "1":
+                spec.render()
+                gen.render()
+                assert spec.last_stats["scan_rtc"] == 1 and gen.last_stats["scan_rtc"] == 0
+        finally:
+            spec.close()
+            gen.close()
