@@ -352,9 +352,11 @@ typedef struct nori_gpu_stats {
     double ms_total;              /* render wall time (host timer)              */
     /* with desc.timing: summed HIP-event time of each kernel, on the launch stream */
     double ms_extend, ms_shadow, ms_shade, ms_splat, ms_finish;
-    /* scan-mode scenes: 1 when the scan kernels run specialised for this scene
-       (hipRTC at nori_gpu_create), the time that compile (or cache read) took
-       then, and 1 when its code object came from the cache */
+    /* scan-mode scenes: 1 when the context holds the scan kernels specialised
+       for this scene (hipRTC at nori_gpu_create; the path integrators' trace
+       launches and the trace API run them, the one-bounce integrators scan
+       generically), the time that compile (or cache read) took then, and 1
+       when its code object came from the cache */
     uint32_t scan_rtc, scan_rtc_cached;
     double ms_scan_rtc;
 } nori_gpu_stats;

@@ -1224,6 +1224,9 @@ int render_one_bounce(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, const std
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->ms_shade = kms[0];  // k_direct: the whole integrator
         stats->ms_splat = kms[1];
+        stats->scan_rtc = c.rtc.extend ? 1u : 0u;  // (held for the trace API; k_direct scans generically)
+        stats->scan_rtc_cached = c.rtc.cached ? 1u : 0u;
+        stats->ms_scan_rtc = c.rtc.compile_ms;
     }
     if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
     return NORI_OK;
