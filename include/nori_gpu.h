@@ -54,9 +54,9 @@ extern "C" {
 #endif
 
 /* Bumped whenever an exported signature or a shared struct changes (6: the
- * leading status argument of nori_gpu_comm_timeout); the Python binding and
- * the C++ adapter refuse a library of another version. */
-#define NORI_GPU_ABI_VERSION 6
+ * leading status argument of nori_gpu_comm_timeout; 7: nori_gpu_stats.nee_inline);
+ * the Python binding and the C++ adapter refuse a library of another version. */
+#define NORI_GPU_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------ */
 #define NORI_OK               0
@@ -341,7 +341,7 @@ typedef struct nori_gpu_stats {
     uint64_t samples;             /* camera samples completed                   */
     uint64_t invalid_samples;     /* NaN/Inf/negative radiance, dropped (block.cpp:94-98) */
     uint64_t rays_closest;        /* extension rays traced by k_extend          */
-    uint64_t rays_shadow;         /* shadow rays traced by k_shadow             */
+    uint64_t rays_shadow;         /* shadow rays traced (k_shadow, or k_shade itself) */
     uint64_t rays_finish;         /* rays traced inside the tail finisher       */
     uint64_t iterations;          /* wavefront iterations                       */
     uint64_t scene_bytes;         /* BVH nodes + primitive records in HBM       */
@@ -359,6 +359,10 @@ typedef struct nori_gpu_stats {
        when its code object came from the cache */
     uint32_t scan_rtc, scan_rtc_cached;
     double ms_scan_rtc;
+    /* 1 when the shade kernel traced its own next-event shadow rays instead of
+       queueing them for k_shadow (scan-mode scenes with the basic plugins by
+       default; NORI_NEE_INLINE=0/1 at nori_gpu_create) */
+    uint32_t nee_inline, reserved0;
 } nori_gpu_stats;
 
 typedef struct nori_gpu_hit {

@@ -91,6 +91,10 @@ struct DevScene {
     // (pair_candidate); trace_cull -- the trace API's scan: 0 tests every
     // pair, 1 the plane-distance skip (plane_may_hit), 2 the in-plane filter
     int32_t camera_cull, trace_cull;
+    // scan-mode scenes: k_shade traces its next-event shadow rays itself
+    // (kernels.hip k_shade) instead of queueing them for k_shadow_scan
+    // (nori_gpu_create: NORI_NEE_INLINE=0 keeps the queue)
+    int32_t nee_inline;
     float root_min[3], root_max[3];  // scene box = BVH root box (bvh.cpp:345)
     int32_t W, H;
     float invW, invH;

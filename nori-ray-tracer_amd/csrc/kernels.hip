@@ -601,6 +601,7 @@ struct ShadowOut {
     V3 o, d, contrib;
     float maxt;
     uint32_t work;
+    bool has_em;  // S.nee_inline: the vertex's emission (nee_em_lds) waits for k_shade's record update
 };
 
 // Sample id of work id w (render.cpp's (pass, pixel) sample; the pcg32 stream
@@ -788,11 +789,29 @@ ND V3 chan_only(const DevScene &S, uint32_t ch, const V3 &a) {
 // ATOMIC false (finisher): the sum is kept in ps.L, in registers -- a tail
 // path's bounces are a serial chain, and a record read per bounce would add a
 // memory latency to each.
+// S.nee_inline (k_shade traces the vertex's shadow ray itself): the emission
+// waits in so.em for the one read-modify-write of the record at the kernel's
+// end, which adds it first and then the unoccluded NEE term -- the order of
+// the adds above.
+// (in LDS by thread, so that it does not hold registers through the rest of
+// the vertex)
+ND float *nee_em_lds() {
+    __shared__ float s_emt[3 * kSeg];
+    return s_emt;
+}
 template <bool ATOMIC>
-ND void rec_add(const DevScene &S, float4 *rec, PathState &ps, const V3 &a0) {
+ND void rec_add(const DevScene &S, float4 *rec, PathState &ps, ShadowOut &so, const V3 &a0) {
     const V3 a = chan_only(S, ps.chan, a0);
     if (!ATOMIC) {
         ps.L = ps.L + a;
+        return;
+    }
+    if (S.nee_inline) {
+        float *const e = nee_em_lds() + 3 * threadIdx.x;
+        e[0] = a.x;
+        e[1] = a.y;
+        e[2] = a.z;
+        so.has_em = true;
         return;
     }
     float *r = reinterpret_cast<float *>(rec + ps.work);
@@ -825,6 +844,7 @@ ND bool skip_nee(const DevScene &S, const DevBsdf &B, const V3 &beta) {
 template <bool ATOMIC, bool FULL = true>
 ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
     so.emit = false;
+    so.has_em = false;
     const uint32_t prim = __float_as_uint(h.y);
     const bool inter = prim != 0xFFFFFFFFu;
     SurfHit hs;
@@ -869,7 +889,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
             w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
         }
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
-        rec_add<ATOMIC>(S, rec, ps, Ladd);
+        rec_add<ATOMIC>(S, rec, ps, so, Ladd);
     }
     if (skip_nee(S, B, ps.beta)) {
         pcg_skip(ps.rng, 3);
@@ -919,6 +939,7 @@ template <int INTEG, bool ATOMIC, bool FULL = true>
 ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *rec, ShadowOut &so) {
     if constexpr (INTEG == NORI_INTEGRATOR_VOLUMETRIC) return shade_vertex_vol<ATOMIC, FULL>(S, ps, h, rec, so);
     so.emit = false;
+    so.has_em = false;
     uint32_t prim = __float_as_uint(h.y);
     if (prim == 0xFFFFFFFFu) return false;  // escaped: path_mis.cpp:84-85
     constexpr bool MIS = INTEG == NORI_INTEGRATOR_PATH_MIS;
@@ -940,7 +961,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         } else {
             Ladd = ps.beta * Le;
         }
-        rec_add<ATOMIC>(S, rec, ps, Ladd);
+        rec_add<ATOMIC>(S, rec, ps, so, Ladd);
     }
     if (MIS && skip_nee(S, B, ps.beta)) {
         pcg_skip3(ps.rng);  // deviation D10: the three NEE draws, unused
@@ -1132,6 +1153,11 @@ ND void next_channel(const DevScene &S, const WorkDesc &wd, PathState &ps) {
 #ifndef NORI_SHADE_WAVES
 #define NORI_SHADE_WAVES 5
 #endif
+// S.nee_inline: one LDS slot per vertex that adds to its record (a shadow ray
+// and/or emission), over the blob: (o, maxt), (d, work | flags),
+// (contrib, the owner thread, whose emission is in nee_em_lds)
+constexpr uint32_t kNeeSlotBytes = kSeg * 3 * 16;
+constexpr uint32_t kSlotEmit = 1u << 31, kSlotEm = 1u << 30;  // above kWorkMask
 #ifndef NORI_SORT_OCTANT
 #define NORI_SORT_OCTANT 1
 #endif
@@ -1150,7 +1176,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     // VAR: 0 basic plugins only (FULL = false), 1 full, 2 full + chromatic
     // aberration (the per-channel continuation is compiled in only then)
     constexpr bool FULL = VAR != 0, CHROMA = VAR == 2;
-    __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64], s_w[kSeg], s_pix[kSeg];
+    __shared__ uint32_t s_sh[kShadeBlock / 64], s_al[kShadeBlock / 64], s_em[kShadeBlock / 64], s_w[kSeg], s_pix[kSeg];
 #if NORI_SORT_OCTANT
     __shared__ uint32_t s_oc[8 * (kShadeBlock / 64)];
     const bool sort_octant = Sg.num_nodes > 0 && Sg.blob_bytes == 0;  // BVH-traversed scenes only
@@ -1194,6 +1220,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     NORI_SPHASE(0)
     ShadowOut so;
     so.emit = false;
+    so.has_em = false;
     bool alive = false;
 #ifdef NORI_PROF_SHADE
     __builtin_amdgcn_s_waitcnt(0);  // path loads landed: phase 1 is the shading proper
@@ -1211,19 +1238,25 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     s_w[tid] = wspec < wd.total ? (uint32_t)wspec : ~0u;
     s_pix[tid] = pspec;
     // ---- compaction: survivors first (in lane order), shadow rays likewise
-    const uint64_t mal = __ballot(alive), msh = __ballot(so.emit);
+    // (S.nee_inline: the vertices that add to their record -- a shadow ray
+    // and/or emission -- into the LDS slots)
+    const bool nee_in = Sg.nee_inline != 0;
+    const bool key = so.emit || so.has_em;  // (has_em only with nee_in)
+    const uint64_t mal = __ballot(alive), msh = __ballot(key), mem = __ballot(so.emit);
     if (lane_id() == 0) {
         s_al[wave] = (uint32_t)__popcll(mal);
         s_sh[wave] = (uint32_t)__popcll(msh);
+        s_em[wave] = (uint32_t)__popcll(mem);
     }
     __syncthreads();
     NORI_SPHASE(2)
-    uint32_t al_off = rank_in(mal), sh_off = rank_in(msh), al_tot = 0, sh_tot = 0;
+    uint32_t al_off = rank_in(mal), sh_off = rank_in(msh), al_tot = 0, sh_tot = 0, em_tot = 0;
     for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
         al_off += w < wave ? s_al[w] : 0u;
         sh_off += w < wave ? s_sh[w] : 0u;
         al_tot += s_al[w];
         sh_tot += s_sh[w];
+        em_tot += s_em[w];
     }
 #if NORI_SORT_OCTANT
     // survivors grouped by the octant of their new direction (then lane
@@ -1248,7 +1281,15 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     }
 #endif
     const uint32_t need_tot = kSeg - al_tot;
-    if (so.emit) {
+    // (the slots overlay the blob: the compaction's barrier above ends every
+    // read of it -- regeneration and the scan below read the global tables)
+    float4 *const s_sa = blob_lds, *const s_sb = s_sa + kSeg, *const s_sc = s_sb + kSeg;
+    if (nee_in && key) {
+        s_sa[sh_off] = make_float4(so.o.x, so.o.y, so.o.z, so.maxt);
+        s_sb[sh_off] = make_float4(so.d.x, so.d.y, so.d.z,
+                                   __uint_as_float(ps.work | (so.emit ? kSlotEmit : 0u) | (so.has_em ? kSlotEm : 0u)));
+        s_sc[sh_off] = make_float4(so.contrib.x, so.contrib.y, so.contrib.z, __uint_as_float(tid));
+    } else if (so.emit) {
         uint32_t i = b * kSeg + sh_off;
         sq.ray_o[i] = make_float4(so.o.x, so.o.y, so.o.z, kEps);
         sq.ray_d[i] = make_float4(so.d.x, so.d.y, so.d.z, so.maxt);
@@ -1265,6 +1306,49 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
             PathState np;
             regen_path<FULL>(Sg, wd, wn, s_pix[tid - al_tot], np, rec);
             store_path(out, q, np);
+        }
+    }
+    if (nee_in) {
+        // slot j = thread j (dense waves): the record is read first, so its
+        // latency hides behind the scan; the shadow ray's any hit through the
+        // wave-uniform scan, as k_shadow_scan; then the record += emission,
+        // += the unoccluded NEE term, in the order of the separate kernels
+        __syncthreads();
+        if (wave * 64u < sh_tot) {
+            const bool mine = tid < sh_tot;
+            const uint32_t j = mine ? tid : 0u;
+            const float4 a = s_sa[j], d = s_sb[j], c = s_sc[j];
+            const uint32_t bits = __float_as_uint(d.w), work = bits & kWorkMask;
+            const bool emit = mine && (bits & kSlotEmit) != 0u, hem = mine && (bits & kSlotEm) != 0u;
+            float4 L = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (mine) L = rec[work];
+            bool f[1] = {false};
+            if (__any(emit)) {
+                TRay r[1];
+                r[0].o = ld3(a);
+                r[0].d = ld3(d);
+                r[0].mint = kEps;
+                r[0].maxt = a.w;
+                bool live[1] = {emit};
+                float t[1], u[1], v[1];
+                uint32_t p[1];
+                scan_rays<1, true>(Sg, r, live, t, p, u, v, f);
+            }
+            bool add = false;
+            if (hem) {
+                const float *e = nee_em_lds() + 3 * __float_as_uint(c.w);
+                L.x += e[0];
+                L.y += e[1];
+                L.z += e[2];
+                add = true;
+            }
+            if (emit && !f[0]) {
+                L.x += c.x;
+                L.y += c.y;
+                L.z += c.z;
+                add = true;
+            }
+            if (add) rec[work] = L;
         }
     }
     NORI_SPHASE(4)
@@ -1287,9 +1371,9 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
         }
         const uint32_t fresh_tot = lo;
         seg.cnt[in_sel ^ 1][b] = al_tot + fresh_tot;
-        seg.shcnt[b] = sh_tot;
+        seg.shcnt[b] = nee_in ? 0u : sh_tot;  // (inline: traced above)
         seg.cursor[b] = cursor + need_tot;
-        seg.stats[b] = make_uint4(st0.x + al_tot + fresh_tot, st0.y + sh_tot, st0.z + fresh_tot, st0.w);
+        seg.stats[b] = make_uint4(st0.x + al_tot + fresh_tot, st0.y + em_tot, st0.z + fresh_tot, st0.w);
         if (stream_work(wd, wd.b0 + b, cursor) < wd.total && stream_work(wd, wd.b0 + b, cursor + need_tot) >= wd.total) {
             // the last segment to run dry tells the host (system-scope store to
             // host-mapped memory) -- no per-iteration readback is needed
@@ -2297,10 +2381,12 @@ static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQue
                            const SegState &seg, int in_sel, const WorkDesc &wd, float4 *rec, Counters *C,
                            uint32_t lds, uint32_t nseg, hipStream_t st) {
     dim3 g(nseg), b(kShadeBlock);  // nseg segments from wd.b0 (wd.G counts the whole pool)
+    // the shadow-ray slots overlay the blob, dead once the vertices are shaded
+    const uint32_t dyn = S.nee_inline ? std::max(lds, kNeeSlotBytes) : lds;
     if (lds)
-        hipLaunchKernelGGL((k_shade<INTEG, true, VAR>), g, b, lds, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
+        hipLaunchKernelGGL((k_shade<INTEG, true, VAR>), g, b, dyn, st, S, in, out, sq, seg, in_sel, wd, rec, C, lds);
     else
-        hipLaunchKernelGGL((k_shade<INTEG, false, VAR>), g, b, 0, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
+        hipLaunchKernelGGL((k_shade<INTEG, false, VAR>), g, b, dyn, st, S, in, out, sq, seg, in_sel, wd, rec, C, 0u);
 }
 template <int INTEG>
 static void shade_dispatch(const DevScene &S, const PathQueue &in, const PathQueue &out, const ShadowQueue &sq,

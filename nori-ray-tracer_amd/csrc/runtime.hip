@@ -951,6 +951,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
     for (int k = 0; k < 3; ++k) S.chromatic[k] = cam.camera_type == NORI_CAMERA_ADVANCED ? cam.chromatic[k] : 0.0f;
     S.chroma = S.chromatic[0] != 0.0f || S.chromatic[1] != 0.0f || S.chromatic[2] != 0.0f;
     S.basic = basic_scene(d) ? 1 : 0;
+    {
+        // shadow rays traced inside k_shade (scan-mode scenes): on by default
+        // for the basic-plugin kernels (C2 +3-7 %, its 64-spp share +3 %), off
+        // for the full ones (C4 -5.7 %, C5 -4.3 %: the full k_shade holds 90-96
+        // VGPRs, and the queue's shadow kernel is the scene-specialised one).
+        // NORI_NEE_INLINE=0 / 1 forces it off / on (for scan-mode scenes).
+        const char *n = std::getenv("NORI_NEE_INLINE");
+        S.nee_inline = c.stack == 0 && (n ? n[0] == '1' : S.basic != 0);
+    }
     S.W_max = cam.width > cam.height ? cam.width : cam.height;
     S.av_length = d.av_length;
     filter_table(cam, S.filter);
@@ -1427,6 +1436,10 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
                                         Gp[h], st);
                 });
                 hipError_t both_err = hipSuccess;
+                if (S.nee_inline) {  // the shadow rays were traced by k_shade itself
+                    timed_on(st, 0, [&] { return launch_extend(S, Qh[h][out], sg.cnt[out], Gp[h], c.stack, st, &c.rtc); });
+                    continue;
+                }
                 if (!timing && c.fuse_trace &&
                     launch_trace_both(S, Qh[h][out], sg.cnt[out], sqh[h], sg.shcnt, c.rec.as<float4>(), Gp[h], c.stack,
                                       &c.rtc, st, both_err)) {
@@ -1597,6 +1610,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         stats->scan_rtc = c.rtc.extend ? 1u : 0u;
         stats->scan_rtc_cached = c.rtc.cached ? 1u : 0u;
         stats->ms_scan_rtc = c.rtc.compile_ms;
+        stats->nee_inline = S.nee_inline ? 1u : 0u;
     }
     if (cancelled) return fail(NORI_ERR_CANCELLED, "rendering was cancelled");
     return NORI_OK;

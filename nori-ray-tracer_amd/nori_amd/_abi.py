@@ -1,4 +1,4 @@
-"""ctypes mirror of include/nori_gpu.h (ABI version 6, _abi.ABI_VERSION).
+"""ctypes mirror of include/nori_gpu.h (ABI version 7, _abi.ABI_VERSION).
 
 The structures below must match the C declarations field for field; the
 test suite checks their sizes against the library (tests/test_abi.py).
@@ -6,7 +6,7 @@ test suite checks their sizes against the library (tests/test_abi.py).
 import ctypes as C
 import os
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 NORI_OK = 0
 NORI_ERR_INVALID = -1
@@ -105,7 +105,8 @@ class Stats(C.Structure):
                 ("path_pool", C.c_uint32), ("ms_total", C.c_double),
                 ("ms_extend", C.c_double), ("ms_shadow", C.c_double), ("ms_shade", C.c_double),
                 ("ms_splat", C.c_double), ("ms_finish", C.c_double),
-                ("scan_rtc", C.c_uint32), ("scan_rtc_cached", C.c_uint32), ("ms_scan_rtc", C.c_double)]
+                ("scan_rtc", C.c_uint32), ("scan_rtc_cached", C.c_uint32), ("ms_scan_rtc", C.c_double),
+                ("nee_inline", C.c_uint32), ("reserved0", C.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
