@@ -1291,7 +1291,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     if (passes == 0 || M == 0) throw NoriException(NORI_ERR_INVALID, "nothing to render (pass_count or blocks empty)");
     const bool one_bounce = S.integrator >= NORI_INTEGRATOR_NORMALS;
     // default pool: about 1/16 of the render's samples in flight, between
-    // 1.5M and 4M paths (~0.9 GB of queues at 4M).  Large pools hide the shade
+    // 1M and 4M paths (~0.9 GB of queues at 4M).  Large pools hide the shade
     // kernel's memory latency (4M measured best among 256K..4M on cbox at 512
     // spp); small renders -- the per-GPU share of a strong-scaled frame --
     // spend less time draining a smaller pool (round 2, two parts, cbox 64
@@ -1299,6 +1299,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // 1 %).  With three parts (round 3) the 64-spp share peaks at 1.25-1.5M
     // (512K 2560, 1M 3030-3160, 1.25M 3320, 1.5M 3275-3296, 2M 3192, 3M 2952)
     // and the 128-spp share at 2M (3989 against 3875 at 2.5M, 3773 at 3M).
+    // Since k_shade traces the shadow rays itself (round 6, nee_inline) the
+    // 64-spp share peaks at 1M again (4875 against 4702 at 1.5M, 4734 at
+    // 1.25M, 4555 at 768K; 3 reps), so the floor is 1M.
     if (one_bounce) return render_one_bounce(c, rd, pixels, blocks, rgbw_out, stats, t0);
     if (M > kWorkMask) throw NoriException(NORI_ERR_INVALID, "frame too large: more than 2^29 pixels per pass");
     uint32_t pool = rd.path_pool;
@@ -1310,7 +1313,6 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
             const uint64_t want = (uint64_t)passes * M / 16;
             pool = 1u << 20;
             while (pool < (1u << 22) && pool < want) pool <<= 1;
-            if (pool < (2u << 20)) pool = 3u << 19;  // 1.5M: measured best for the 64-spp share (3 parts)
         }
     }
     pool = std::max<uint32_t>(kSeg, (pool + kSeg - 1) / kSeg * kSeg);
