@@ -31,6 +31,14 @@ constexpr int kScanRaysShadow = NORI_SCAN_RAYS_SHADOW;  // ... and of the scan-m
 #define NORI_SHADE_LDS_MAX 16384
 #endif
 constexpr uint32_t kShadeLdsMax = NORI_SHADE_LDS_MAX;  // largest scene blob the shade kernel stages in LDS
+// The shade kernels of the full plugin set are compiled without the inline
+// shadow rays (S.nee_inline only for basic scenes): with them, C4 3964 and
+// C5 4162 against 4000 / 4308 Msamples/s, queue mode both (one box, 2 reps).
+// NORI_NEE_FULL=1 compiles them in (NORI_NEE_INLINE=1 then applies there too).
+#ifndef NORI_NEE_FULL
+#define NORI_NEE_FULL 0
+#endif
+constexpr bool kNeeFull = NORI_NEE_FULL;
 
 struct SplatDesc {
     uint32_t M;               // pixels per pass in the work list

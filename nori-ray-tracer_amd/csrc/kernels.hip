@@ -799,14 +799,14 @@ ND float *nee_em_lds() {
     __shared__ float s_emt[3 * kSeg];
     return s_emt;
 }
-template <bool ATOMIC>
+template <bool ATOMIC, bool INL>
 ND void rec_add(const DevScene &S, float4 *rec, PathState &ps, ShadowOut &so, const V3 &a0) {
     const V3 a = chan_only(S, ps.chan, a0);
     if (!ATOMIC) {
         ps.L = ps.L + a;
         return;
     }
-    if (S.nee_inline) {
+    if (INL && S.nee_inline) {
         float *const e = nee_em_lds() + 3 * threadIdx.x;
         e[0] = a.x;
         e[1] = a.y;
@@ -889,7 +889,7 @@ ND bool shade_vertex_vol(const DevScene &S, PathState &ps, const float4 &h, floa
             w = ps.prev + pe > 0.f ? ps.prev / (ps.prev + pe) : ps.prev;
         }
         const V3 Ladd = ((ps.beta * w) * Le) * medium_tr(S, hs.p, hs.p);
-        rec_add<ATOMIC>(S, rec, ps, so, Ladd);
+        rec_add<ATOMIC, !FULL || kNeeFull>(S, rec, ps, so, Ladd);
     }
     if (skip_nee(S, B, ps.beta)) {
         pcg_skip(ps.rng, 3);
@@ -961,7 +961,7 @@ ND bool shade_vertex(const DevScene &S, PathState &ps, const float4 &h, float4 *
         } else {
             Ladd = ps.beta * Le;
         }
-        rec_add<ATOMIC>(S, rec, ps, so, Ladd);
+        rec_add<ATOMIC, !FULL || kNeeFull>(S, rec, ps, so, Ladd);
     }
     if (MIS && skip_nee(S, B, ps.beta)) {
         pcg_skip3(ps.rng);  // deviation D10: the three NEE draws, unused
@@ -1240,7 +1240,7 @@ void k_shade(DevScene Sg, PathQueue in, PathQueue out, ShadowQueue sq, SegState 
     // ---- compaction: survivors first (in lane order), shadow rays likewise
     // (S.nee_inline: the vertices that add to their record -- a shadow ray
     // and/or emission -- into the LDS slots)
-    const bool nee_in = Sg.nee_inline != 0;
+    const bool nee_in = (!FULL || kNeeFull) && Sg.nee_inline != 0;
     const bool key = so.emit || so.has_em;  // (has_em only with nee_in)
     const uint64_t mal = __ballot(alive), msh = __ballot(key), mem = __ballot(so.emit);
     if (lane_id() == 0) {

@@ -956,9 +956,10 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         // for the basic-plugin kernels (C2 +3-7 %, its 64-spp share +3 %), off
         // for the full ones (C4 -5.7 %, C5 -4.3 %: the full k_shade holds 90-96
         // VGPRs, and the queue's shadow kernel is the scene-specialised one).
-        // NORI_NEE_INLINE=0 / 1 forces it off / on (for scan-mode scenes).
+        // NORI_NEE_INLINE=0 / 1 forces it off / on for scan-mode scenes whose
+        // shade kernel carries it (the basic ones; kernels.h kNeeFull).
         const char *n = std::getenv("NORI_NEE_INLINE");
-        S.nee_inline = c.stack == 0 && (n ? n[0] == '1' : S.basic != 0);
+        S.nee_inline = c.stack == 0 && (n ? n[0] == '1' : S.basic != 0) && (S.basic != 0 || kNeeFull);
     }
     S.W_max = cam.width > cam.height ? cam.width : cam.height;
     S.av_length = d.av_length;

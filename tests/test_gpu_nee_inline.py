@@ -4,12 +4,14 @@ any hit through the wave-uniform scan, then one read-modify-write of each
 sample record -- emission first, then the unoccluded NEE term, the order of
 the separate k_shadow_scan launch) against the shadow queue
 (NORI_NEE_INLINE=0): the same image up to the film sums' order, the same ray
-counts, for each integrator that traces shadow rays (path_mis, volumetric),
-for path_mats (emission only), and for the full and chromatic-aberration
-shade variants, which run the queue by default.  The default switches are
-checked too: on for the basic-plugin Cornell box, off for the full-plugin
-volumetric scene and for BVH scenes."""
+counts, for each integrator that traces shadow rays (path_mis, volumetric)
+and for path_mats (emission only).  Only the basic-plugin shade kernels
+carry the inline path (kernels.h kNeeFull): on scenes with the full plugin
+set (point lights, Disney, chromatic aberration) NORI_NEE_INLINE=1 keeps
+the queue.  The defaults are checked too: on for the basic-plugin Cornell
+box, off for the full-plugin volumetric scene and for BVH scenes."""
 import os
+import re
 
 import numpy as np
 import pytest
@@ -40,8 +42,15 @@ def _renderer(s, **env):
 def _scene(kind, tmp_path):
     if kind == "cbox_path_mis":
         return nori_amd.load_scene(scene_path("pa4", "cbox", "cbox_path_mis.xml"), 96, 72, 8)
-    if kind == "volumetric":
-        return nori_amd.load_scene(scene_path("project", "volumetric", "volumetric.xml"), 80, 60, 8)
+    if kind in ("volumetric", "volumetric_basic"):
+        src = open(scene_path("project", "volumetric", "volumetric.xml")).read()
+        src = src.replace('value="meshes/', f'value="{scene_path("project", "volumetric", "meshes")}/')
+        if kind == "volumetric_basic":  # the Disney sphere made diffuse: the basic plugin set
+            src = re.sub(r'<bsdf type="disney">.*?</bsdf>',
+                         '<bsdf type="diffuse"><color name="albedo" value="0.5 0.5 0.5"/></bsdf>', src, flags=re.S)
+        xml = str(tmp_path / f"{kind}.xml")
+        open(xml, "w").write(src)
+        return nori_amd.load_scene(xml, 80, 60, 8)
     if kind in ("path_mats", "lights_path_mis"):
         extra = ""
         if kind == "lights_path_mis":
@@ -56,14 +65,17 @@ def _scene(kind, tmp_path):
     return nori_amd.load_scene(xml, 0, 0, 8)
 
 
-@pytest.mark.parametrize("kind", ["cbox_path_mis", "path_mats", "lights_path_mis", "volumetric", "chroma_path_mis"])
+BASIC = ["cbox_path_mis", "path_mats", "volumetric_basic"]
+
+
+@pytest.mark.parametrize("kind", BASIC + ["lights_path_mis", "volumetric", "chroma_path_mis"])
 def test_inline_nee_same_image(built, tmp_path, kind):
     s = _scene(kind, tmp_path)
     inl, que = _renderer(s, NORI_NEE_INLINE="1"), _renderer(s, NORI_NEE_INLINE="0")
     try:
         a, b = inl.render(), que.render()
         sa, sb = inl.last_stats, que.last_stats
-        assert sa["nee_inline"] == 1 and sb["nee_inline"] == 0
+        assert sa["nee_inline"] == (1 if kind in BASIC else 0) and sb["nee_inline"] == 0
         assert np.allclose(a, b, rtol=1e-5, atol=1e-6), np.abs(a - b).max()
         for k in ("samples", "invalid_samples", "rays_closest", "rays_shadow", "rays_finish"):
             assert sa[k] == sb[k], (k, sa[k], sb[k])
