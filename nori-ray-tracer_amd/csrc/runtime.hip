@@ -209,7 +209,7 @@ struct nori_gpu_ctx {
     DevScene S{};
     ScanRtc rtc;         // scan-mode scenes: the scan kernels specialised for this scene (rtc.hip), or empty
     // an iteration's extension and shadow rays of a part in one launch
-    // (launch_trace_both); NORI_TRACE_FUSE=0 at creation: two launches
+    // (launch_trace_both); set at upload_scene (NORI_TRACE_FUSE=0 / 1 forces it)
     bool fuse_trace = true;
     // the tail's finisher enqueued before the film splat beside it (NORI_FINISH_FIRST=0: after)
     bool finish_first = true;
@@ -960,6 +960,15 @@ void upload_scene(nori_gpu_ctx &c, const nori_scene_desc &d) {
         // shade kernel carries it (the basic ones; kernels.h kNeeFull).
         const char *n = std::getenv("NORI_NEE_INLINE");
         S.nee_inline = c.stack == 0 && (n ? n[0] == '1' : S.basic != 0) && (S.basic != 0 || kNeeFull);
+    }
+    {
+        // one launch for an iteration's extension and shadow queues: on for
+        // the BVH walks (C3 +10 %) and the basic scan kernels that keep the
+        // queue; the full-plugin scan scenes run faster with two launches
+        // (C4 3942 -> 3957, C5 4217 -> 4288 Msamples/s, 3 interleaved reps,
+        // tools/gpu_fuse_ab.sh).  NORI_TRACE_FUSE=0 / 1 forces it.
+        const char *f = std::getenv("NORI_TRACE_FUSE");
+        c.fuse_trace = f ? f[0] != '0' : !(c.stack == 0 && S.basic == 0);
     }
     S.W_max = cam.width > cam.height ? cam.width : cam.height;
     S.av_length = d.av_length;
@@ -1878,7 +1887,6 @@ int nori_gpu_create(const nori_scene_desc *d, int device, nori_gpu_ctx **out) {
         std::unique_ptr<nori_gpu_ctx> c(new nori_gpu_ctx);
         c->device = device;
         c->spp = d->sample_count ? d->sample_count : 1;
-        if (const char *e = std::getenv("NORI_TRACE_FUSE"); e && e[0] == '0') c->fuse_trace = false;
         if (const char *e = std::getenv("NORI_FINISH_FIRST"); e && e[0] == '0') c->finish_first = false;
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));

@@ -148,10 +148,10 @@ def test_camera_cull_render_equal(built, parts):
 @pytest.mark.parametrize("traversal", ["scan", "bvh"])
 def test_fused_trace_launch_same_image(built, parts, traversal):
     """One launch for an iteration's extension and shadow rays (nori_rtc_trace_both /
-    k_trace_both) against the two separate launches (NORI_TRACE_FUSE=0): the same
+    k_trace_both; NORI_TRACE_FUSE=1) against the two separate launches (=0): the same
     image up to the film sums' order, in both traversal modes."""
     s = nori_amd.load_scene(scene_path(*parts), 96, 72, 8)
-    fused, split = (_renderer(s, NORI_TRAVERSAL=traversal),
+    fused, split = (_renderer(s, NORI_TRAVERSAL=traversal, NORI_TRACE_FUSE="1"),
                     _renderer(s, NORI_TRAVERSAL=traversal, NORI_TRACE_FUSE="0"))
     try:
         fa, fb = fused.render(), split.render()
