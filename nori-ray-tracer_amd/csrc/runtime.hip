@@ -1311,7 +1311,9 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
     // and the 128-spp share at 2M (3989 against 3875 at 2.5M, 3773 at 3M).
     // Since k_shade traces the shadow rays itself (round 6, nee_inline) the
     // 64-spp share peaks at 1M again (4875 against 4702 at 1.5M, 4734 at
-    // 1.25M, 4555 at 768K; 3 reps), so the floor is 1M.
+    // 1.25M, 4555 at 768K; 3 reps), so the floor is 1M.  The BVH walks
+    // (C3) want about 1/8 in flight: 4M 846-851 against 807-812 at 2M
+    // (3M 796-798, 6M 796-798, 8M 839-846; 3 interleaved reps).
     if (one_bounce) return render_one_bounce(c, rd, pixels, blocks, rgbw_out, stats, t0);
     if (M > kWorkMask) throw NoriException(NORI_ERR_INVALID, "frame too large: more than 2^29 pixels per pass");
     uint32_t pool = rd.path_pool;
@@ -1320,7 +1322,7 @@ int render(nori_gpu_ctx &c, const nori_gpu_render_desc &rd, float *rgbw_out, nor
         if (e && std::atol(e) > 0) {
             pool = (uint32_t)std::min<long>(std::atol(e), 1L << 26);
         } else {
-            const uint64_t want = (uint64_t)passes * M / 16;
+            const uint64_t want = (uint64_t)passes * M / (c.stack ? 8 : 16);
             pool = 1u << 20;
             while (pool < (1u << 22) && pool < want) pool <<= 1;
         }
